@@ -1,0 +1,67 @@
+// ref_harness.cpp -- TEST INFRASTRUCTURE ONLY.  Links the UNMODIFIED reference core
+// (/root/reference/src/{environment,map,player,cards,geometry}.cpp + its headers) and exposes a
+// tiny C API so tests/golden generation can drive the reference's own vec_cog_env<1> and
+// vec_action_sampler<1> (include/vec_environment.h, include/vec_sampler.h).
+//
+// Built by oracle/Makefile into oracle/_ref/libref.so with the image's clang++ against the
+// image's libstdc++ 11; no shims, stand-in headers or patched libraries.  Consequence: the
+// reference ABORTS on seeds whose map generation erases past the end of valid_indices
+// (map.cpp:727, behaviour that needs GCC>=13 libstdc++) and on 2/3-player B-start maps
+// (map.cpp:347-352).  Callers must screen seeds with the C oracle's hazard flags first.
+#include "vec_environment.h"
+#include "vec_sampler.h"
+#include <cstdint>
+#include <cstring>
+
+using env1 = vec_cog_env<1>;
+using smp1 = vec_action_sampler<1>;
+
+extern "C" {
+void *ref_create() { return new env1(); }
+void ref_destroy(void *h) { delete static_cast<env1 *>(h); }
+int ref_reset(void *h, uint32_t seed, uint8_t np, uint8_t npieces, int diff, uint32_t max_steps) {
+  try {
+    static_cast<env1 *>(h)->reset(seed, np, npieces, static_cast<Difficulty>(diff), max_steps, false);
+  } catch (const generate_map_failure &) {
+    return -1;
+  }
+  return 0;
+}
+int ref_reset_default(void *h) {
+  try {
+    static_cast<env1 *>(h)->reset();
+  } catch (const generate_map_failure &) {
+    return -1;
+  }
+  return 0;
+}
+int ref_step(void *h, const void *action) {
+  try {
+    static_cast<env1 *>(h)->step(*reinterpret_cast<const std::array<ActionData, 1> *>(action));
+  } catch (const generate_map_failure &) {
+    return -1;
+  }
+  return 0;
+}
+const void *ref_obs(void *h) { return static_cast<env1 *>(h)->get_observations().data(); }
+const void *ref_sel(void *h) { return static_cast<env1 *>(h)->get_selected_action_masks().data(); }
+const void *ref_rewards(void *h) { return static_cast<env1 *>(h)->get_rewards().data(); }
+const void *ref_dones(void *h) { return static_cast<env1 *>(h)->get_dones().data(); }
+const void *ref_agent(void *h) { return static_cast<env1 *>(h)->get_agent_selections().data(); }
+const void *ref_infos(void *h) { return static_cast<env1 *>(h)->get_infos().data(); }
+size_t ref_sizeof(int which) {
+  switch (which) {
+  case 0: return sizeof(ObsData);
+  case 1: return sizeof(ActionMask);
+  case 2: return sizeof(ActionData);
+  case 3: return sizeof(Info);
+  default: return 0;
+  }
+}
+void *ref_sampler_create(uint32_t seed) { return new smp1(seed); }
+void ref_sampler_destroy(void *s) { delete static_cast<smp1 *>(s); }
+void ref_sample(void *s, const void *mask) {
+  static_cast<smp1 *>(s)->sample(*reinterpret_cast<const std::array<ActionMask, 1> *>(mask));
+}
+const void *ref_sampler_actions(void *s) { return static_cast<smp1 *>(s)->get_actions().data(); }
+}
