@@ -1,0 +1,85 @@
+"""In-tree build of the engine for gfx950 (no pip install; the .so files travel with the repo).
+
+    python gym-eldorado_amd/build_ext.py          # library + bindings (+ oracle checkers)
+
+Outputs (git-ignored, shipped to the GPU box by the snapshot):
+    gym-eldorado_amd/city_of_gold/libcog_hip.so          HIP kernels + C ABI (hipcc, gfx950)
+    gym-eldorado_amd/city_of_gold/_city_of_gold*.so      pybind11 host module (links the above)
+    oracle/liboracle.so                                  C oracle (test infrastructure only)
+    oracle/_ref/libref.so                                reference core (only where /root/reference exists)
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import sysconfig
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+OUT = os.path.join(PKG, "city_of_gold")
+INCLUDE = os.path.join(ROOT, "include")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("COG_OFFLOAD_ARCH", "gfx950")
+
+LIB = os.path.join(OUT, "libcog_hip.so")
+EXT = os.path.join(OUT, "_city_of_gold" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+ENGINE_SRCS = [os.path.join(CSRC, f) for f in ("cog_engine.hip", "cog_abi.cpp")]
+ENGINE_DEPS = ENGINE_SRCS + [os.path.join(CSRC, f) for f in ("cog_engine.h", "cog_tables.h")] + [
+    os.path.join(INCLUDE, f) for f in ("cog.h", "cog_types.h")]
+EXT_SRCS = [os.path.join(CSRC, "pybind_module.cpp")]
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd, cwd=None):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True, cwd=cwd)
+
+
+def build_engine(force=False):
+    if force or _stale(LIB, ENGINE_DEPS):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+              "-ffp-contract=off", "-Wall", f"-I{INCLUDE}", f"-I{CSRC}", *ENGINE_SRCS, "-o", LIB])
+    return LIB
+
+
+def build_bindings(force=False):
+    import pybind11
+
+    if force or _stale(EXT, EXT_SRCS + [LIB, os.path.join(INCLUDE, "cog.h"), os.path.join(INCLUDE, "cog_types.h")]):
+        cxx = os.environ.get("CXX", "g++")
+        _run([cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-fvisibility=hidden",
+              f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", f"-I{INCLUDE}",
+              *EXT_SRCS, "-o", EXT, f"-L{OUT}", "-lcog_hip", "-Wl,-rpath,$ORIGIN"])
+    return EXT
+
+
+def build_oracle():
+    """Checkers only (tests / smoke / bench cpu_baseline); never linked by the product."""
+    _run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "all"])
+    if os.path.isdir("/root/reference/src"):
+        _run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "oracle"), "ref"])
+
+
+def build_all(force=False, oracle=True):
+    build_engine(force)
+    build_bindings(force)
+    if oracle:
+        build_oracle()
+
+
+def add_to_path():
+    if PKG not in sys.path:
+        sys.path.insert(0, PKG)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

@@ -1,0 +1,105 @@
+"""city_of_gold -- MI355X-native drop-in for the reference `city_of_gold` pybind11 module.
+
+Same surface as the reference (src/pybind/common.cpp:5-37, src/pybind/vectorized.cpp:8-21,
+include/pybind/vectorized.h:163-275):
+
+    import city_of_gold as cg
+    envs = cg.vec.get_vec_env(N)()           # class vec_cog_env_N
+    samplers = cg.vec.get_vec_sampler(N)(seed)
+    runner = cg.vec.get_runner(N)(envs, samplers, n_threads)
+    envs.reset(seed, 4, 3, cg.Difficulty.EASY, 100000, False)
+
+Differences, all additive: any N is accepted (the reference stops at 256 and only offers
+N in {0..8, 16, 32, ..., 256}); input arrays are length/record-size checked (ValueError instead
+of an out-of-bounds read); views keep their owner alive.  Runners accept two extra keyword
+arguments: device_views=True keeps outputs in HBM (no per-sync host copy) and
+stored_masks=True samples from the current agent's stored mask (full game dynamics).
+
+All computation runs in libcog_hip.so on a gfx950 GPU.  There is no CPU fallback: creating an
+environment without a usable device raises RuntimeError.
+"""
+from __future__ import annotations
+
+import sys
+import types
+
+from . import _city_of_gold as _C
+
+Difficulty = _C.Difficulty
+EASY, MEDIUM, HARD = _C.EASY, _C.MEDIUM, _C.HARD
+ObsData, ActionMask, ActionData, Info, DeckObs = _C.ObsData, _C.ActionMask, _C.ActionData, _C.Info, _C.DeckObs
+device_count = _C.device_count
+
+VEC_ENV_CLS = "vec_cog_env_"
+VEC_SAMPLER_CLS = "vec_sampler_"
+VEC_RUNNER_CLS = "vec_runner_"
+
+vec = types.ModuleType("city_of_gold.vec", "Vectorized utilities")
+# Q28: the reference binds samplers into `vec.env` and envs into `vec.sampler`
+# (include/pybind/vectorized.h:260-273, call order vs. parameter names); the getters are right.
+vec.env = types.ModuleType("city_of_gold.vec.env", "Vectorized environments")
+vec.sampler = types.ModuleType("city_of_gold.vec.sampler", "Vectorized action samplers")
+vec.runner = types.ModuleType("city_of_gold.vec.runner", "Vectorized runners")
+for _m in (vec, vec.env, vec.sampler, vec.runner):
+    sys.modules[_m.__name__] = _m
+
+
+def _check_n(n):
+    if isinstance(n, bool) or not isinstance(n, int) or n < 0:
+        raise TypeError("number of environments must be a non-negative int")
+    return int(n)
+
+
+def _make_env_cls(n):
+    def __init__(self, device=None):
+        _C.VecEnvBase.__init__(self, n, device)
+
+    doc = (f"Vectorized city of gold environment for {n} environments.\n\n"
+           "reset() must be called first to initialize the environments before stepping.")
+    return type(VEC_ENV_CLS + str(n), (_C.VecEnvBase,), {"__init__": __init__, "__doc__": doc,
+                                                         "__module__": "city_of_gold.vec.sampler"})
+
+
+def _make_sampler_cls(n):
+    def __init__(self, seed=None, device=None):
+        _C.VecSamplerBase.__init__(self, n, seed, device)
+
+    return type(VEC_SAMPLER_CLS + str(n), (_C.VecSamplerBase,), {"__init__": __init__,
+                                                                 "__module__": "city_of_gold.vec.env"})
+
+
+def _make_runner_cls(n):
+    def __init__(self, env, sampler, n_threads=None, device_views=False, stored_masks=False):
+        if env.num_envs != n:
+            raise ValueError(f"runner for {n} envs got an env batch of {env.num_envs}")
+        _C.RunnerBase.__init__(self, env, sampler, n_threads, device_views, stored_masks)
+
+    return type(VEC_RUNNER_CLS + str(n), (_C.RunnerBase,), {"__init__": __init__,
+                                                            "__module__": "city_of_gold.vec.runner"})
+
+
+def _getter(module, prefix, factory):
+    def get(n):
+        n = _check_n(n)
+        name = prefix + str(n)
+        cls = getattr(module, name, None)
+        if cls is None:
+            cls = factory(n)
+            setattr(module, name, cls)
+        return cls
+
+    return get
+
+
+get_vec_env = _getter(vec.sampler, VEC_ENV_CLS, _make_env_cls)
+get_vec_sampler = _getter(vec.env, VEC_SAMPLER_CLS, _make_sampler_cls)
+get_runner = _getter(vec.runner, VEC_RUNNER_CLS, _make_runner_cls)
+vec.get_vec_env, vec.get_vec_sampler, vec.get_runner = get_vec_env, get_vec_sampler, get_runner
+
+# pre-create the reference's instantiations (vectorized.h:260-267: 0..8, 16, 32, ..., 256)
+for _n in list(range(0, 9)) + [16, 32, 64, 128, 256]:
+    get_vec_env(_n), get_vec_sampler(_n), get_runner(_n)
+del _n, _m
+
+__all__ = ["vec", "Difficulty", "EASY", "MEDIUM", "HARD", "ObsData", "ActionMask", "ActionData", "Info",
+           "DeckObs", "get_vec_env", "get_vec_sampler", "get_runner", "device_count"]

@@ -1,0 +1,110 @@
+// cog_engine.h -- internal interface between the C-ABI layer (cog_abi.cpp) and the CDNA4 kernels
+// (cog_engine.hip).  Not part of the public ABI.
+//
+// Device data layout per environment i (all buffers allocated once per handle, in HBM):
+//   obs   [N] x 17216 B   ObsData records, byte-identical to reference api.h:126-129 -- THE
+//                         engine state for everything the reference keeps in ObsData (decks,
+//                         stored masks, phase, resources, shop) and the map encode target.
+//   sel   [N] x 128 B     selected ActionMask (the deck's mask, player.cpp:16-27)
+//   info  [N] x 192 B     Info records
+//   rew   [N] x 4 f32, done [N] u8, agent [N] u8
+//   priv  [N] x 128 B     EnvPriv: everything the reference keeps in private members
+//                         (rng, turn counter, Player/Deck/Shop counters, player locations,
+//                         map bounds) -- one 128-B line per env
+//   grid  [N] x 16384 B   absolute-coordinate hex-code grid, 128 x 128 cells, cell (x, y) at
+//                         (x + 64) * 128 + (y + 64); 0 = no hex.  Built by map generation,
+//                         read by movement masks, done checks and the map-observation encode.
+//   gen   [N] x 256 B     map-generation scratch (pieces list, per-env piece transforms)
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/cog_types.h"
+
+namespace cog {
+
+constexpr int kGridDim = 128;
+constexpr int kGridOff = 64;
+constexpr int kGridBytes = kGridDim * kGridDim;
+constexpr int kMaxCoord = 62;        // |x|,|y| of any placed hex; beyond -> hazard GRID_OVER
+constexpr int kMaxPlaced = 96;       // pieces placed in one generation (incl. recursion)
+
+// hazard / status flags (same bit meaning as the oracle's ORC_F_*)
+constexpr uint32_t F_MAPGEN_FAIL = 0x01u;
+constexpr uint32_t F_ERASE_PAST = 0x02u;
+constexpr uint32_t F_Q9_OOB = 0x04u;
+constexpr uint32_t F_Q24_CLAMP = 0x08u;
+constexpr uint32_t F_GRID_OVER = 0x10u;
+constexpr uint32_t F_OOB_LOOKUP = 0x20u;
+constexpr uint32_t F_SCAN_OVER = 0x40u;
+constexpr uint32_t F_B_START_LT4 = 0x80u;
+constexpr uint32_t F_ERROR_MASK = F_MAPGEN_FAIL | F_GRID_OVER;
+
+struct PlayerPriv {                  // Player + Deck private members (player.h:60-75, cards.h:137-145)
+  uint8_t has_won, mip, n_removes, next_card_free;
+  uint8_t next_move_free, n_in_hand, n_active, n_in_draw;
+  uint8_t idx_last, steps_taken, n_added_cards, pad;
+  uint32_t n_movements;
+};
+
+struct alignas(64) EnvPriv {         // cog_env private members (environment.h:12-33) + Map/Shop state
+  uint32_t rng;                      // env minstd_rand0 state
+  uint32_t seed;
+  uint32_t max_steps;
+  uint32_t turn_counter;
+  uint8_t n_players, n_pieces, difficulty, done;
+  uint8_t agent, n_in_market, loc_size, render;
+  uint32_t in_market;                // Shop::in_market bits
+  uint32_t flags;                    // sticky hazard flags
+  int8_t minx, miny, maxx, maxy;     // Map::min_xy / max_xy (integer hex coords)
+  uint8_t dimx, dimy, need_encode, pad0;
+  int8_t locx[4], locy[4];           // Map::player_locations
+  uint32_t pad1[4];
+  PlayerPriv pl[4];
+};
+static_assert(sizeof(EnvPriv) == 128, "EnvPriv is one 128-B line");
+
+struct alignas(64) GenScratch {
+  uint8_t pieces[kMaxPlaced];
+  int16_t pcx[20], pcy[20];          // piece centres (doubled coords)
+  uint8_t prot[20];                  // piece rotations mod 6
+  uint8_t npieces, pad[11];
+};
+static_assert(sizeof(GenScratch) <= 256, "GenScratch");
+
+struct DevState {
+  size_t n;
+  uint8_t *obs;
+  uint8_t *sel;
+  uint8_t *info;
+  float *rew;
+  uint8_t *done;
+  uint8_t *agent;
+  EnvPriv *priv;
+  uint8_t *grid;
+  GenScratch *gen;
+  uint32_t *status;                  // [0] OR of error flags, [1] error count, [2] dirty count
+  uint32_t *dirty;                   // [n] envs whose map was re-generated (host view refresh)
+};
+
+struct ResetParams {
+  uint32_t seed;
+  uint8_t n_players, n_pieces, difficulty, use_params;   // use_params=0: cog_env::reset()
+  uint32_t max_steps;
+};
+
+enum MaskSource : int { MASK_SELECTED = 0, MASK_STORED = 1, MASK_EXTERNAL = 2 };
+
+// host-side launchers (stream = hipStream_t passed as void*)
+int launch_init(const DevState &s, const uint32_t *seeds_host_unused, uint32_t default_seed,
+                void *stream);
+int launch_reset(const DevState &s, const ResetParams &p, void *stream);
+int launch_encode_all(const DevState &s, void *stream);
+int launch_step(const DevState &s, const uint8_t *d_actions, void *stream);
+int launch_sample(size_t n, const uint8_t *d_masks, uint32_t *d_rng, uint8_t *d_actions,
+                  void *stream);
+int launch_sample_step(const DevState &s, int mask_source, uint32_t *d_rng, uint8_t *d_actions,
+                       void *stream);
+int launch_seed_sampler(size_t n, uint32_t seed, uint32_t *d_rng, void *stream);
+
+}  // namespace cog

@@ -1,0 +1,1074 @@
+// cog_engine.hip -- CDNA4 (gfx950) kernels of the batched City-of-Gold engine.
+//
+// One work-item owns one environment for the whole step (the per-env work is a short,
+// branchy integer state machine over ~1 KB of state; there is no GEMM and no MFMA use).
+// State lives in HBM in the layout documented in cog_engine.h: the reference's own ObsData /
+// ActionMask / Info records (so host and device views are the engine state, no write-back
+// pass) plus one 128-B private line per env and a 128x128 hex-code grid per env.
+//
+// Semantics follow the reference line by line (citations per function); the representation
+// does not: hex geometry is exact integer arithmetic on a doubled lattice
+// (rot+1: (x, y) -> (-y, x + y), the exact value of geometry.cpp:3-17 + map.cpp:17-37 on this
+// lattice) and overlap tests use the occupancy grid instead of sort+merge (map.cpp:53-74).
+//
+// Kernels:
+//   k_init           default-construct N envs (vec_environment.h:23-30)
+//   k_reset          cog_env::reset(params) incl. procedural map generation (map.cpp:697-742)
+//   k_encode         48x48x7 map-observation encode (map.cpp:389-405): streaming, 1 WG / env
+//   k_sample         masked uniform sampler (sampler.h:14-79)
+//   k_step           vec_cog_env::step with auto-reset (vec_environment.h:46-61)
+//   k_sample_step    runner-fused sample(selected|stored masks) + step (runner.h:46-55)
+#include <hip/hip_runtime.h>
+
+#include "cog_engine.h"
+#include "cog_tables.h"
+
+#define DEV __device__ __forceinline__
+
+namespace cog {
+
+__constant__ cog_card_t c_cards[COG_N_CARDTYPES] = COG_CARD_TABLE;
+__constant__ uint8_t c_shop_types[COG_N_SHOP] = COG_SHOP_TYPES;
+__constant__ cog_piece_meta_t c_pmeta[COG_N_PIECES] = COG_PIECE_META;
+__constant__ uint8_t c_phex[COG_N_PIECES][37] = COG_PIECE_HEX;
+__constant__ int8_t c_large[37][2] = COG_LARGE_XY2;
+__constant__ int8_t c_small[16][2] = COG_SMALL_XY2;
+__constant__ int8_t c_end[3][2] = COG_END_XY2;
+__constant__ int8_t c_dirs[7][2] = COG_DIRS_XY2;
+__constant__ int8_t c_conn_ll[2][2] = COG_CONN_LL_XY2;
+__constant__ int8_t c_conn_ls[3][2] = COG_CONN_LS_XY2;
+__constant__ int8_t c_conn_lt[1][2] = COG_CONN_LT_XY2;
+__constant__ int8_t c_conn_sl[6][2] = COG_CONN_SL_XY2;
+__constant__ int8_t c_opts_range[6] = {-2, -1, 0, 1, 2, 3};
+__constant__ int8_t c_opts_ls[2] = {-1, 2};
+__constant__ int8_t c_opts_lt[1] = {-3};
+
+// shop slots that start in the market (cards.cpp:85-92 / 94-100): slots 0,1,5,7,9,12
+constexpr uint32_t kInMarket0 = (1u << 0) | (1u << 1) | (1u << 5) | (1u << 7) | (1u << 9) | (1u << 12);
+
+// ------------------------------------------------------------------------------------------
+// RNG: minstd_rand0 and libstdc++ uniform_int_distribution<size_t> downscaling
+// ------------------------------------------------------------------------------------------
+DEV uint32_t mr_seed(uint64_t s) {
+  uint32_t x = (uint32_t)(s % 2147483647ull);
+  return x == 0 ? 1u : x;
+}
+DEV uint32_t mr_next(uint32_t &x) {
+  const uint64_t p = (uint64_t)x * 16807u;                 // < 2^46
+  uint32_t r = (uint32_t)(p & 0x7fffffffu) + (uint32_t)(p >> 31);
+  r = r >= 0x7fffffffu ? r - 0x7fffffffu : r;
+  x = r;
+  return r;
+}
+// uniform integer in [0, k-1], k >= 1 (uniform_int_distribution<size_t>(0, k-1))
+DEV uint32_t uid(uint32_t &x, uint32_t k) {
+  const uint32_t scaling = 2147483645u / k;
+  const uint32_t past = k * scaling;
+  uint32_t r;
+  do {
+    r = mr_next(x) - 1u;
+  } while (r >= past);
+  return r / scaling;
+}
+
+// ------------------------------------------------------------------------------------------
+// per-env context
+// ------------------------------------------------------------------------------------------
+struct Ctx {
+  uint8_t *ob;        // ObsData record
+  uint8_t *sel;       // selected ActionMask
+  uint8_t *info;      // Info record
+  float *rew;         // rewards[4]
+  EnvPriv *pv;        // private state
+  uint8_t *grid;      // 128x128 hex codes
+  GenScratch *gs;
+};
+
+DEV Ctx make_ctx(const DevState &s, size_t i) {
+  Ctx e;
+  e.ob = s.obs + i * COG_OBS_BYTES;
+  e.sel = s.sel + i * COG_MASK_BYTES;
+  e.info = s.info + i * COG_INFO_BYTES;
+  e.rew = s.rew + i * 4;
+  e.pv = s.priv + i;
+  e.grid = s.grid + i * (size_t)kGridBytes;
+  e.gs = s.gen + i;
+  return e;
+}
+
+DEV uint8_t *deck(const Ctx &e, int p) { return e.ob + COG_OBS_PLAYER0 + COG_OBS_PLAYER_STRIDE * p; }
+DEV uint8_t *stm(const Ctx &e, int p) { return deck(e, p) + COG_PD_MASK; }
+DEV float *res(const Ctx &e) { return reinterpret_cast<float *>(e.ob + COG_OBS_RES); }
+DEV bool is_special(int c) { return c >= 15 && c <= 20; }
+
+DEV uint8_t grid_at(const uint8_t *g, int x, int y) { return g[(x + kGridOff) * kGridDim + (y + kGridOff)]; }
+
+// Map::get_from_array (map.cpp:273-275) on absolute integer coords
+DEV uint8_t lookup(const Ctx &e, int x, int y) {
+  EnvPriv *pv = e.pv;
+  const int ix = x - pv->minx + 1, iy = y - pv->miny + 1;
+  if (ix < 0 || iy < 0 || ix >= pv->dimx || iy >= pv->dimy) {
+    pv->flags |= F_OOB_LOOKUP;
+    return COG_HEX_MOUNTAIN;
+  }
+  const uint8_t c = grid_at(e.grid, x, y);
+  return c ? c : (uint8_t)COG_HEX_MOUNTAIN;
+}
+
+// ------------------------------------------------------------------------------------------
+// Deck / Player / Shop (cards.cpp:94-294, player.cpp:29-206)
+// ------------------------------------------------------------------------------------------
+DEV int scan(const Ctx &e, const uint8_t *d, int base, uint32_t t) {
+  int c = 0;
+  while (t >= d[base + c]) {
+    t -= d[base + c];
+    ++c;
+    if (base + c >= 105) {
+      e.pv->flags |= F_SCAN_OVER;
+      return c;
+    }
+  }
+  return c;
+}
+
+DEV void move_discard_to_draw(const Ctx &e, int p) {      // cards.cpp:234-240
+  uint8_t *d = deck(e, p);
+  PlayerPriv &P = e.pv->pl[p];
+  uint8_t nd = P.n_in_draw;
+  for (int i = 0; i < COG_N_CARDTYPES; i++) {
+    const uint8_t x = d[COG_DECK_DISCARD + i];
+    d[COG_DECK_DRAW + i] = (uint8_t)(d[COG_DECK_DRAW + i] + x);
+    nd = (uint8_t)(nd + x);
+    d[COG_DECK_DISCARD + i] = 0;
+  }
+  P.n_in_draw = nd;
+}
+
+DEV void deck_draw(const Ctx &e, int p, uint8_t n) {        // cards.cpp:183-211
+  PlayerPriv &P = e.pv->pl[p];
+  uint8_t *d = deck(e, p);
+  if (P.n_in_draw < n) move_discard_to_draw(e, p);
+  if (n > P.n_in_draw) n = P.n_in_draw;
+  uint32_t rng = e.pv->rng;
+  for (int i = 0; i < n; i++) {
+    const uint32_t t = uid(rng, P.n_in_draw);
+    const int c = scan(e, d, COG_DECK_DRAW, t);
+    d[COG_DECK_DRAW + c]--;
+    P.n_in_draw--;
+    d[COG_DECK_HAND + c]++;
+    e.sel[COG_MASK_PLAY + 1 + c] = 1;
+    e.sel[COG_MASK_SPECIAL + 1 + c] = is_special(c);
+  }
+  e.pv->rng = rng;
+  P.n_in_hand = (uint8_t)(P.n_in_hand + n);
+}
+
+DEV void deck_activate(const Ctx &e, int p, int c) {        // cards.cpp:242-253
+  PlayerPriv &P = e.pv->pl[p];
+  uint8_t *d = deck(e, p);
+  P.n_in_hand--;
+  P.n_active++;
+  P.idx_last = (uint8_t)c;
+  const uint8_t prev = d[COG_DECK_HAND + c];
+  d[COG_DECK_HAND + c] = (uint8_t)(prev - 1);
+  d[COG_DECK_ACTIVE + c]++;
+  const uint8_t pl = prev > 1;
+  e.sel[COG_MASK_PLAY + 1 + c] = pl;
+  e.sel[COG_MASK_SPECIAL + 1 + c] = pl && is_special(c);
+}
+
+DEV void deck_play_last_activated(const Ctx &e, int p) {    // cards.cpp:255-261
+  PlayerPriv &P = e.pv->pl[p];
+  uint8_t *d = deck(e, p);
+  P.n_active--;
+  d[COG_DECK_ACTIVE + P.idx_last]--;
+  if (!c_cards[P.idx_last].single_use) d[COG_DECK_PLAYED + P.idx_last]++;
+}
+
+DEV void deck_play_immediate(const Ctx &e, int p, int c) {  // cards.cpp:263-273
+  PlayerPriv &P = e.pv->pl[p];
+  uint8_t *d = deck(e, p);
+  P.n_in_hand--;
+  const uint8_t prev = d[COG_DECK_HAND + c];
+  d[COG_DECK_HAND + c] = (uint8_t)(prev - 1);
+  d[COG_DECK_PLAYED + c]++;
+  const uint8_t pl = prev > 1;
+  e.sel[COG_MASK_PLAY + 1 + c] = pl;
+  e.sel[COG_MASK_SPECIAL + 1 + c] = pl && is_special(c);
+}
+
+DEV void deck_remove_immediate(const Ctx &e, int p, int c) { // cards.cpp:281-290
+  PlayerPriv &P = e.pv->pl[p];
+  uint8_t *d = deck(e, p);
+  P.n_in_hand--;
+  const uint8_t prev = d[COG_DECK_HAND + c];
+  d[COG_DECK_HAND + c] = (uint8_t)(prev - 1);
+  e.sel[COG_MASK_REMOVE + 1 + c] = e.sel[COG_MASK_REMOVE + 1 + c] && prev > 1;
+  const uint8_t pl = e.sel[COG_MASK_PLAY + 1 + c] && prev > 1;
+  e.sel[COG_MASK_PLAY + 1 + c] = pl;
+  e.sel[COG_MASK_SPECIAL + 1 + c] = pl && is_special(c);
+}
+
+DEV void disable_playing(const Ctx &e) {                    // player.cpp:191-196
+  for (int k = 0; k < 22; k++) {
+    e.sel[COG_MASK_PLAY + k] = k == 0;
+    e.sel[COG_MASK_SPECIAL + k] = k == 0;
+  }
+}
+
+DEV void enable_playing(const Ctx &e, int p) {              // player.cpp:198-206
+  const uint8_t *d = deck(e, p);
+  e.sel[COG_MASK_REMOVE] = 1;
+  for (int k = 1; k < 22; k++) {
+    e.sel[COG_MASK_REMOVE + k] = 0;
+    const uint8_t pl = d[COG_DECK_HAND + k - 1] > 0;
+    e.sel[COG_MASK_PLAY + k] = pl;
+    e.sel[COG_MASK_SPECIAL + k] = pl && is_special(k - 1);
+  }
+}
+
+DEV void cards_from_active(const Ctx &e, int p, uint8_t n, bool discard) {  // player.cpp:85-131
+  PlayerPriv &P = e.pv->pl[p];
+  uint8_t *d = deck(e, p);
+  const uint8_t avail = P.n_active;
+  if (n > avail) {
+    if (discard) e.pv->flags |= F_Q24_CLAMP;
+    n = avail;
+  }
+  uint32_t rng = e.pv->rng;
+  for (uint8_t i = 0; i < n; i++) {
+    const uint32_t t = uid(rng, (uint32_t)(avail - i));
+    const int c = scan(e, d, COG_DECK_ACTIVE, t);
+    P.n_active--;
+    d[COG_DECK_ACTIVE + c]--;
+    if (discard) d[COG_DECK_DISCARD + c]++;
+  }
+  e.pv->rng = rng;
+}
+
+DEV void handle_requirement(const Ctx &e, int p, int req, uint8_t n) {  // player.cpp:141-162
+  PlayerPriv &P = e.pv->pl[p];
+  float *r = res(e);
+  if (req < 3) {
+    const float left = r[req] - (float)n;
+    r[0] = 0.f; r[1] = 0.f; r[2] = 0.f;
+    r[req] = left;
+    if (!P.mip) {
+      deck_play_last_activated(e, p);
+      P.mip = 1;
+    }
+  } else if (req == COG_REQ_REMOVE || req == COG_REQ_DISCARD) {
+    cards_from_active(e, p, n, req == COG_REQ_DISCARD);
+    r[0] = 0.f; r[1] = 0.f; r[2] = 0.f;
+    P.mip = 0;
+  }
+}
+
+DEV void copy_mask(uint8_t *dst, const uint8_t *src) {     // ActionMask copy (named fields)
+  const uint4 *s = reinterpret_cast<const uint4 *>(src);
+  uint4 *d = reinterpret_cast<uint4 *>(dst);
+#pragma unroll
+  for (int k = 0; k < 6; k++) d[k] = s[k];                 // bytes 0..95 (92 named + pad)
+}
+
+DEV void end_turn(const Ctx &e, int p) {                   // player.cpp:170-180
+  PlayerPriv &P = e.pv->pl[p];
+  uint8_t *d = deck(e, p);
+  P.n_active = 0;
+  for (int i = 0; i < COG_N_CARDTYPES; i++) {
+    d[COG_DECK_DISCARD + i] = (uint8_t)(d[COG_DECK_DISCARD + i] + d[COG_DECK_ACTIVE + i]);
+    d[COG_DECK_ACTIVE + i] = 0;
+  }
+  for (int i = 0; i < COG_N_CARDTYPES; i++) {
+    d[COG_DECK_DISCARD + i] = (uint8_t)(d[COG_DECK_DISCARD + i] + d[COG_DECK_PLAYED + i]);
+    d[COG_DECK_PLAYED + i] = 0;
+  }
+  const int n_draw = COG_HAND_SIZE - (int)P.n_in_hand;
+  if (n_draw > 0) deck_draw(e, p, (uint8_t)n_draw);
+  float *r = res(e);
+  r[0] = 0.f; r[1] = 0.f; r[2] = 0.f;
+  copy_mask(stm(e, p), e.sel);
+}
+
+DEV void shop_mask(const Ctx &e, float coins, uint8_t *mask) {  // cards.cpp:109-121
+  const uint8_t *avail = e.ob + COG_OBS_SHOP;
+  const uint32_t im = e.pv->in_market;
+  const bool few = e.pv->n_in_market < COG_MKT_SLOTS;
+  for (int i = 0; i < COG_N_SHOP; i++) {
+    const float cost = (float)c_cards[c_shop_types[i]].cost;
+    const bool ok = few ? avail[i] > 0 : ((im >> i) & 1u);
+    mask[i + 1] = ok && (coins > cost);
+  }
+}
+
+DEV int shop_get(const Ctx &e, int k) {                    // cards.cpp:136-142
+  uint8_t *avail = e.ob + COG_OBS_SHOP;
+  const uint8_t a = (uint8_t)(avail[k] - 1);
+  avail[k] = a;
+  if (!a && ((e.pv->in_market >> k) & 1u)) {
+    e.pv->in_market &= ~(1u << k);
+    e.pv->n_in_market--;
+  }
+  return c_shop_types[k];
+}
+
+DEV void movement_mask(const Ctx &e, uint8_t *move, int player, const float *r, uint8_t n_active) {
+  // map.cpp:369-387
+  const int lx = e.pv->locx[player], ly = e.pv->locy[player];
+#pragma unroll
+  for (int i = 1; i < 7; i++) {
+    const uint8_t c = lookup(e, lx + c_dirs[i][0] / 2, ly + c_dirs[i][1] / 2);
+    const int req = COG_HEX_REQ(c);
+    bool filled;
+    if (req >= COG_REQ_DISCARD) filled = n_active > COG_HEX_N(c);
+    else filled = r[req] >= (float)COG_HEX_N(c);
+    move[i] = (req != COG_REQ_NULL) && filled;
+  }
+}
+
+DEV void update_observation(const Ctx &e, int agent) {     // environment.cpp:252-279
+  uint8_t *am = stm(e, agent);
+  am[COG_MASK_MOVE] = 1;
+  for (int k = 1; k < 7; k++) am[COG_MASK_MOVE + k] = 0;
+  am[COG_MASK_SHOP] = 1;
+  for (int k = 1; k < 19; k++) am[COG_MASK_SHOP + k] = 0;
+  const uint8_t ph = e.ob[COG_OBS_PHASE];
+  if (ph == COG_PHASE_MOVEMENT) {
+    float r[3] = {res(e)[0], res(e)[1], res(e)[2]};
+    movement_mask(e, am + COG_MASK_MOVE, agent, r, e.pv->pl[agent].n_active);
+  } else if (ph == COG_PHASE_BUYING) {
+    shop_mask(e, res(e)[2], am + COG_MASK_SHOP);
+  }
+}
+
+DEV void player_reset(const Ctx &e, int p) {               // player.cpp:29-43
+  PlayerPriv &P = e.pv->pl[p];
+  uint8_t *d = deck(e, p);
+  P.has_won = 0; P.mip = 0; P.next_card_free = 0; P.next_move_free = 0;
+  P.n_removes = 0; P.steps_taken = 0; P.n_movements = 0; P.n_added_cards = 0;
+  for (int k = 0; k < COG_N_CARDTYPES; k++) {              // DeckObs::reset keeps `played` (Q10)
+    d[COG_DECK_DRAW + k] = 0; d[COG_DECK_HAND + k] = 0;
+    d[COG_DECK_ACTIVE + k] = 0; d[COG_DECK_DISCARD + k] = 0;
+  }
+  for (int k = 0; k < 22; k++) {                           // ActionMask::reset (api.h:104-118)
+    e.sel[COG_MASK_PLAY + k] = k == 0;
+    e.sel[COG_MASK_REMOVE + k] = k == 0;
+    e.sel[COG_MASK_SPECIAL + k] = k == 0;
+  }
+  e.sel[COG_MASK_MOVE] = 1;
+  e.sel[COG_MASK_SHOP] = 1;
+  d[COG_DECK_DISCARD + 0] = 3;                             // Deck::reset (cards.cpp:163-171)
+  d[COG_DECK_DISCARD + 7] = 4;
+  d[COG_DECK_DISCARD + 5] = 1;
+  P.n_in_draw = 0; P.n_in_hand = 0; P.n_active = 0;
+  deck_draw(e, p, COG_HAND_SIZE);
+  copy_mask(stm(e, p), e.sel);
+}
+
+// special actions (cards.cpp:8-36) and the remove-lambda (environment.cpp:156-158), applied to
+// the stored mask of the CURRENT agent and the ACTING player (environment.cpp:183-186)
+DEV void apply_special(const Ctx &e, int special, int p) {
+  uint8_t *mask = stm(e, e.pv->agent);
+  PlayerPriv &P = e.pv->pl[p];
+  switch (special) {
+    case COG_SPECIAL_DRAW2: deck_draw(e, p, 2); break;
+    case COG_SPECIAL_DRAW3: deck_draw(e, p, 3); break;
+    case COG_SPECIAL_DRAW1_REMOVE1:
+    case COG_SPECIAL_DRAW2_REMOVE2: {
+      const uint8_t k = special == COG_SPECIAL_DRAW1_REMOVE1 ? 1 : 2;
+      deck_draw(e, p, k);
+      P.n_removes = k;
+      for (int j = 0; j < 22; j++) mask[COG_MASK_REMOVE + j] = mask[COG_MASK_PLAY + j];
+      disable_playing(e);
+      shop_mask(e, 0.f, mask + COG_MASK_SHOP);
+    } break;
+    case COG_SPECIAL_TRANSMIT:
+      mask[COG_MASK_MOVE] = 1;
+      for (int k = 1; k < 7; k++) mask[COG_MASK_MOVE + k] = 0;
+      disable_playing(e);
+      for (int i = 0; i < COG_N_SHOP; i++) mask[COG_MASK_SHOP + 1 + i] = e.ob[COG_OBS_SHOP + i] > 0;
+      P.next_card_free = 1;
+      break;
+    case COG_SPECIAL_NATIVE: {
+      const float r100[3] = {100.f, 100.f, 100.f};
+      movement_mask(e, mask + COG_MASK_MOVE, p, r100, 100);
+      P.next_move_free = 1;
+      disable_playing(e);
+      shop_mask(e, 0.f, mask + COG_MASK_SHOP);
+    } break;
+    case COG_SPECIAL_SHOP_OFF: shop_mask(e, 0.f, mask + COG_MASK_SHOP); break;
+    default: break;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Procedural map generation (map.cpp:17-74, 154-341, 697-752) on the doubled integer lattice
+// ------------------------------------------------------------------------------------------
+DEV void rot_pt(int t, int X, int Y, int &ox, int &oy) {   // rotate by t*60 degrees, t in [0,6)
+  switch (t) {
+    case 0: ox = X; oy = Y; break;
+    case 1: ox = -Y; oy = X + Y; break;
+    case 2: ox = -X - Y; oy = X; break;
+    case 3: ox = -X; oy = -Y; break;
+    case 4: ox = Y; oy = -X - Y; break;
+    default: ox = X + Y; oy = -X; break;
+  }
+}
+DEV int norm6(int t) {
+  t %= 6;
+  return t < 0 ? t + 6 : t;
+}
+DEV void piece_xy2(int piece, int k, int &X, int &Y) {
+  const int sz = c_pmeta[piece].size;
+  if (sz == COG_PS_LARGE) { X = c_large[k][0]; Y = c_large[k][1]; }
+  else if (sz == COG_PS_SMALL) { X = c_small[k][0]; Y = c_small[k][1]; }
+  else { X = c_end[k][0]; Y = c_end[k][1]; }
+}
+
+DEV void map_reset(const Ctx &e) {                         // map.cpp:744-752
+  EnvPriv *pv = e.pv;
+  for (int x = pv->minx; x <= pv->maxx; x++)
+    for (int y = pv->miny; y <= pv->maxy; y++) e.grid[(x + kGridOff) * kGridDim + (y + kGridOff)] = 0;
+  pv->minx = pv->miny = pv->maxx = pv->maxy = 0;
+  pv->dimx = pv->dimy = 0;
+  e.gs->npieces = 0;
+}
+
+// MapPiece::rotate + translate, then Map::add_piece bookkeeping (map.cpp:179-191, 309-341)
+DEV bool add_piece(const Ctx &e, int p, int cx2, int cy2, int rot) {
+  GenScratch *gs = e.gs;
+  EnvPriv *pv = e.pv;
+  const int r = norm6(gs->prot[p] + rot);
+  gs->prot[p] = (uint8_t)r;
+  const int pcx = gs->pcx[p] + cx2, pcy = gs->pcy[p] + cy2;
+  gs->pcx[p] = (int16_t)pcx;
+  gs->pcy[p] = (int16_t)pcy;
+  if (gs->npieces >= kMaxPlaced) {
+    pv->flags |= F_GRID_OVER;
+    return false;
+  }
+  gs->pieces[gs->npieces++] = (uint8_t)p;
+  int mnx = pv->minx, mny = pv->miny, mxx = pv->maxx, mxy = pv->maxy;
+  const int nh = c_pmeta[p].n_hex;
+  for (int k = 0; k < nh; k++) {
+    int X, Y, rx, ry;
+    piece_xy2(p, k, X, Y);
+    rot_pt(r, X, Y, rx, ry);
+    rx += pcx;
+    ry += pcy;
+    if ((rx | ry) & 1) {                                   // never on valid lattices
+      pv->flags |= F_GRID_OVER;
+      return false;
+    }
+    const int x = rx / 2, y = ry / 2;
+    if (x < -kMaxCoord || x > kMaxCoord || y < -kMaxCoord || y > kMaxCoord) {
+      pv->flags |= F_GRID_OVER;
+      return false;
+    }
+    e.grid[(x + kGridOff) * kGridDim + (y + kGridOff)] = c_phex[p][k];
+    mxx = max(mxx, x); mxy = max(mxy, y);
+    mnx = min(mnx, x); mny = min(mny, y);
+  }
+  pv->minx = (int8_t)mnx; pv->miny = (int8_t)mny;
+  pv->maxx = (int8_t)mxx; pv->maxy = (int8_t)mxy;
+  return true;
+}
+
+// footprint of piece p (reset state) rotated by t and centred at (cx2, cy2) hits no placed hex?
+DEV bool footprint_free(const Ctx &e, int p, int t, int cx2, int cy2) {
+  const int nh = c_pmeta[p].n_hex;
+  for (int k = 0; k < nh; k++) {
+    int X, Y, rx, ry;
+    piece_xy2(p, k, X, Y);
+    rot_pt(t, X, Y, rx, ry);
+    rx += cx2;
+    ry += cy2;
+    if ((rx | ry) & 1) continue;                           // off-lattice point: cannot coincide
+    const int x = rx / 2, y = ry / 2;
+    if (x < -kGridOff || x >= kGridOff || y < -kGridOff || y >= kGridOff) continue;
+    if (grid_at(e.grid, x, y)) return false;
+  }
+  return true;
+}
+
+struct ConnSet {
+  const int8_t (*base)[2];
+  const int8_t *opts;
+  int nbase, nopt, copies;
+};
+
+// MapPiece::get_ref_connection_points (map.cpp:203-263): what placed piece q offers to `psize`
+DEV bool conn_set(int q, int psize, ConnSet &cs) {
+  const int qs = c_pmeta[q].size, qk = c_pmeta[q].kind;
+  if (qs == COG_PS_LARGE) {
+    if (psize == COG_PS_LARGE) { cs.base = c_conn_ll; cs.nbase = 2; cs.opts = c_opts_range; cs.nopt = 6; cs.copies = 7; return true; }
+    if (psize == COG_PS_SMALL) { cs.base = c_conn_ls; cs.nbase = 3; cs.opts = c_opts_ls; cs.nopt = 2; cs.copies = 7; return true; }
+    if (psize == COG_PS_TRIPLE && qk != COG_PT_START) { cs.base = c_conn_lt; cs.nbase = 1; cs.opts = c_opts_lt; cs.nopt = 1; cs.copies = 7; return true; }
+    return false;
+  }
+  if (qs == COG_PS_SMALL && psize == COG_PS_LARGE) {
+    cs.base = c_conn_sl; cs.nbase = 6; cs.opts = c_opts_range; cs.nopt = 6; cs.copies = 1;
+    return true;
+  }
+  return false;
+}
+
+// Map::add_random_piece (map.cpp:277-307): two passes over the candidate list instead of
+// materialising it (count the valid ones, draw, find the chosen one again)
+DEV bool add_random_piece(const Ctx &e, int p, uint32_t &rng) {
+  GenScratch *gs = e.gs;
+  gs->pcx[p] = 0; gs->pcy[p] = 0; gs->prot[p] = 0;         // MapPiece::reset
+  const int psize = c_pmeta[p].size;
+  const int npl = gs->npieces;
+  uint32_t chosen = 0xffffffffu;
+  uint32_t nvalid = 0;
+  for (int pass = 0; pass < 2; pass++) {
+    uint32_t count = 0;
+    for (int qi = 0; qi < npl; qi++) {
+      const int q = gs->pieces[qi];
+      ConnSet cs;
+      if (!conn_set(q, psize, cs)) continue;
+      const int qcx = gs->pcx[q], qcy = gs->pcy[q], qrot = gs->prot[q];
+      for (int ci = 0; ci < cs.copies; ci++) {
+        for (int j = 0; j < cs.nbase; j++) {
+          int cx, cy;
+          rot_pt(norm6(ci + qrot), cs.base[j][0], cs.base[j][1], cx, cy);
+          cx += qcx;
+          cy += qcy;
+          const int opt0 = cs.opts[0] + ci + qrot;
+          if (!footprint_free(e, p, norm6(opt0), cx, cy)) continue;
+          if (pass == 1 && count == chosen) {
+            const uint32_t ri = uid(rng, (uint32_t)cs.nopt);
+            const int rot = cs.opts[ri] + ci + qrot;
+            return add_piece(e, p, cx, cy, rot);
+          }
+          count++;
+        }
+      }
+    }
+    if (pass == 0) {
+      nvalid = count;
+      if (!nvalid) return false;
+      chosen = uid(rng, nvalid);
+    }
+  }
+  return false;  // unreachable
+}
+
+DEV bool finalize_ok(const Ctx &e) {                       // map.cpp:389-405 (dims check, Q27)
+  EnvPriv *pv = e.pv;
+  const int dx = 3 + pv->maxx - pv->minx, dy = 3 + pv->maxy - pv->miny;
+  if (dx > 49 || dy > 49) {
+    pv->flags |= F_GRID_OVER;
+    return false;
+  }
+  pv->dimx = (uint8_t)dx;
+  pv->dimy = (uint8_t)dy;
+  return true;
+}
+
+struct GenFrame {
+  uint32_t rng;
+  uint8_t i, nvalid, stage, pad;
+  uint8_t valid[16];
+};
+
+// Map::generate (map.cpp:697-742) as an explicit-stack state machine.  A frame's rng is its own
+// copy (the reference passes the engine by value), recursion depth == failures.
+DEV bool generate(const Ctx &e) {
+  enum { ENTER = 0, LOOP = 1, END = 2, FIN = 3 };
+  EnvPriv *pv = e.pv;
+  GenFrame fr[COG_MAX_FAILURES];
+  int depth = 0;
+  fr[0].rng = pv->rng;
+  fr[0].stage = ENTER;
+  const int n_pieces = pv->n_pieces, diff = pv->difficulty;
+  while (depth >= 0) {
+    GenFrame &F = fr[depth];
+    if (F.stage == ENTER) {
+      const uint32_t s = uid(F.rng, 2);
+      if (!add_piece(e, COG_PIECE_START0 + (int)s, 0, 0, 0)) return false;
+      F.nvalid = 0;
+      for (int i = 0; i < COG_N_TRAVEL; i++)
+        if (c_pmeta[COG_PIECE_TRAVEL0 + i].difficulty <= diff) F.valid[F.nvalid++] = (uint8_t)i;
+      F.i = 0;
+      F.stage = LOOP;
+    } else if (F.stage == LOOP) {
+      if (F.i < n_pieces) {
+        bool ok = false;
+        int next = 0;
+        if (F.nvalid) {
+          next = F.valid[uid(F.rng, F.nvalid)];
+          ok = add_random_piece(e, COG_PIECE_TRAVEL0 + next, F.rng);
+          if (pv->flags & F_GRID_OVER) return false;
+        }
+        F.i++;
+        if (ok) {
+          // vector::erase(begin() + next) with GCC>=13 libstdc++ semantics (Q5)
+          const int num = (int)F.nvalid - (next + 1);
+          for (int k = 0; k < num; k++) F.valid[next + k] = F.valid[next + 1 + k];
+          if (next >= F.nvalid) pv->flags |= F_ERASE_PAST;
+          F.nvalid--;
+        } else {
+          if (depth + 1 >= COG_MAX_FAILURES) return false;
+          fr[depth + 1].rng = F.rng;
+          fr[depth + 1].stage = ENTER;
+          depth++;
+        }
+      } else {
+        F.stage = END;
+      }
+    } else if (F.stage == END) {
+      const uint32_t en = uid(F.rng, 2);
+      F.stage = FIN;
+      const bool ok = add_random_piece(e, COG_PIECE_END0 + (int)en, F.rng);
+      if (pv->flags & F_GRID_OVER) return false;
+      if (!ok) {
+        map_reset(e);
+        if (depth + 1 >= COG_MAX_FAILURES) return false;
+        fr[depth + 1].rng = F.rng;
+        fr[depth + 1].stage = ENTER;
+        depth++;
+      }
+    } else {
+      if (!finalize_ok(e)) return false;
+      depth--;
+    }
+  }
+  return true;
+}
+
+DEV void add_players(const Ctx &e) {                       // map.cpp:343-354 (Q9 defined)
+  EnvPriv *pv = e.pv;
+  const int n = pv->n_players;
+  if (n < pv->loc_size) {
+    pv->loc_size = (uint8_t)n;
+  } else {
+    for (int k = pv->loc_size; k < n && k < 4; k++) { pv->locx[k] = 0; pv->locy[k] = 0; }
+    pv->loc_size = (uint8_t)n;
+  }
+  const int start = e.gs->pieces[0];
+  for (int i = 0; i < 37; i++) {
+    const uint8_t c = c_phex[start][i];
+    const int ps = COG_HEX_REQ(c) == COG_REQ_NULL ? COG_HEX_N(c) : 0;
+    if (ps > 0 && ps < n + 1) {
+      if (i < pv->loc_size && i < 4) {
+        pv->locx[i] = (int8_t)(c_large[i][0] / 2);
+        pv->locy[i] = (int8_t)(c_large[i][1] / 2);
+      } else {
+        pv->flags |= F_Q9_OOB;
+      }
+    }
+  }
+  if (start == COG_PIECE_START0 + 1 && n < 4) pv->flags |= F_B_START_LT4;
+}
+
+// cog_env::reset() (environment.cpp:42-64)
+DEV bool env_reset(const Ctx &e) {
+  EnvPriv *pv = e.pv;
+  pv->agent = 0;
+  e.ob[COG_OBS_PHASE] = COG_PHASE_INACTIVE;
+  map_reset(e);
+  GenScratch *gs = e.gs;
+  for (int p = 0; p < COG_N_PIECES; p++) { gs->pcx[p] = 0; gs->pcy[p] = 0; gs->prot[p] = 0; }
+  if (!generate(e)) {
+    pv->flags |= F_MAPGEN_FAIL;
+    return false;
+  }
+  for (int i = 0; i < pv->n_players; i++) player_reset(e, i);
+  add_players(e);
+  for (int k = 0; k < COG_N_SHOP; k++) e.ob[COG_OBS_SHOP + k] = COG_CARDS_PER_TYPE;
+  pv->in_market = kInMarket0;                              // n_in_market NOT reset (Q12)
+  pv->done = 0;
+  pv->turn_counter = 0;
+  for (int i = 0; i < pv->n_players; i++) update_observation(e, i);
+  copy_mask(e.sel, stm(e, 0));
+  pv->need_encode = 1;
+  return true;
+}
+
+// cog_env::step (environment.cpp:91-224)
+DEV void env_step(const Ctx &e, const uint8_t *act) {
+  EnvPriv *pv = e.pv;
+  if (pv->done) return;
+  const uint8_t a_play = act[0], a_special = act[1], a_remove = act[2], a_move = act[3], a_shop = act[4];
+  const int ag = pv->agent;
+  e.info[COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag]++;  // agent_infos[a].steps_taken (u8)
+  if (e.ob[COG_OBS_PHASE] == COG_PHASE_INACTIVE) e.ob[COG_OBS_PHASE] = COG_PHASE_MOVEMENT;
+  PlayerPriv &P = pv->pl[ag];
+  P.steps_taken++;
+  float *r = res(e);
+  int special = COG_SPECIAL_NONE;
+  if (a_play) {
+    const int c = (uint8_t)(a_play - 1);
+    const uint8_t ph = e.ob[COG_OBS_PHASE];
+    if (ph == COG_PHASE_MOVEMENT) {
+      r[0] = (float)c_cards[c].res[0]; r[1] = (float)c_cards[c].res[1]; r[2] = (float)c_cards[c].res[2];
+    } else if (ph == COG_PHASE_BUYING) {
+      const uint8_t coin = c_cards[c].res[2];
+      r[2] = r[2] + (coin > 0 ? (float)coin : 0.5f);
+    }
+    deck_activate(e, ag, c);
+  } else if (a_special) {
+    const int c = (uint8_t)(a_special - 1);
+    if (c_cards[c].single_use) deck_remove_immediate(e, ag, c);
+    else deck_play_immediate(e, ag, c);
+    special = c_cards[c].special;
+  } else if (a_move) {
+    const int nx = pv->locx[ag] + c_dirs[a_move][0] / 2, ny = pv->locy[ag] + c_dirs[a_move][1] / 2;
+    pv->locx[ag] = (int8_t)nx;
+    pv->locy[ag] = (int8_t)ny;
+    const uint8_t c = lookup(e, nx, ny);
+    if (!P.next_move_free) handle_requirement(e, ag, COG_HEX_REQ(c), COG_HEX_N(c));
+    else { P.next_move_free = 0; enable_playing(e, ag); }
+    P.n_movements++;
+    P.has_won = COG_HEX_END(c);
+  } else {
+    P.next_move_free = 0;
+    if (a_shop) {
+      const int k = (uint8_t)(a_shop - 1);
+      int type;
+      if (P.next_card_free) {
+        type = shop_get(e, k);
+      } else {
+        const uint32_t was = (pv->in_market >> k) & 1u;
+        pv->n_in_market = (uint8_t)(pv->n_in_market + (uint8_t)(1u - was));
+        pv->in_market |= 1u << k;
+        type = shop_get(e, k);
+        r[2] = r[2] - (float)c_cards[type].cost;
+        e.ob[COG_OBS_PHASE] = (uint8_t)((e.ob[COG_OBS_PHASE] + 1) % 3);
+      }
+      deck(e, ag)[COG_DECK_DISCARD + type]++;
+      P.n_added_cards++;
+    } else if (a_remove) {
+      deck_remove_immediate(e, ag, (uint8_t)(a_remove - 1));
+      P.n_removes--;
+      if (!P.n_removes) enable_playing(e, ag);
+      else special = COG_SPECIAL_SHOP_OFF;
+    } else {
+      e.ob[COG_OBS_PHASE] = (uint8_t)((e.ob[COG_OBS_PHASE] + 1) % 3);
+      if (P.n_removes > 0) { P.n_removes = 0; enable_playing(e, ag); }
+    }
+    if (P.next_card_free) { P.next_card_free = 0; enable_playing(e, ag); }
+  }
+  if (P.mip && !a_move) {
+    P.mip = 0;
+    r[0] = 0.f; r[1] = 0.f; r[2] = 0.f;
+  }
+  if (P.has_won || e.ob[COG_OBS_PHASE] == COG_PHASE_INACTIVE) {  // maybe_end_turn / next_agent
+    end_turn(e, ag);
+    uint8_t na = (uint8_t)(pv->agent + 1);
+    if (na >= pv->n_players) na = 0;
+    pv->agent = na;
+    copy_mask(e.sel, stm(e, na));
+    r[0] = 0.f; r[1] = 0.f; r[2] = 0.f;
+    pv->turn_counter++;
+  }
+  const int cur = pv->agent;
+  update_observation(e, cur);
+  if (special != COG_SPECIAL_NONE) {
+    apply_special(e, special, ag);
+  } else {
+    const uint8_t c = lookup(e, pv->locx[cur], pv->locy[cur]);
+    if (COG_HEX_END(c) || pv->turn_counter >= pv->max_steps) {
+      pv->done = 1;
+      *reinterpret_cast<uint32_t *>(e.info) = pv->turn_counter;
+      float n_winners = 0.f;
+      for (int q = 0; q < 4; q++) n_winners += (float)pv->pl[q].has_won;
+      for (int q = 0; q < pv->n_players; q++) {
+        const PlayerPriv &Q = pv->pl[q];
+        uint8_t *ai = e.info + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * q;
+        const float rw = (float)(pv->n_players * Q.has_won) - n_winners;
+        ai[0] = Q.steps_taken;
+        *reinterpret_cast<float *>(ai + 4) = rw;
+        *reinterpret_cast<uint32_t *>(ai + 8) = Q.n_movements;
+        ai[12] = Q.n_added_cards;
+        ai[13] = Q.n_added_cards;                          // get_n_removed (player.cpp:223-224)
+        *reinterpret_cast<uint32_t *>(ai + 16) = 0u;       // n_spent never incremented (Q14)
+        *reinterpret_cast<uint32_t *>(ai + 20) = 0u;
+        *reinterpret_cast<uint32_t *>(ai + 24) = 0u;
+        *reinterpret_cast<uint32_t *>(ai + 28) = Q.n_added_cards;
+        e.rew[q] = rw;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// map-observation encode (map.cpp:389-405): feature 0 stays 0 (Q2), f[req+1] = n, f[6] = is_end
+// ------------------------------------------------------------------------------------------
+DEV uint32_t feat_byte(uint8_t code, int f) {
+  if (!code || f == 0) return 0;
+  if (f == 6) return COG_HEX_END(code);
+  const int req = COG_HEX_REQ(code);
+  return (req != COG_REQ_NULL && f == req + 1) ? COG_HEX_N(code) : 0u;
+}
+
+struct EncGeom {
+  int minx, miny, dimx, dimy;
+};
+
+DEV uint8_t cell_code(const uint8_t *g, const EncGeom &eg, int c) {
+  if (c >= COG_GRID * COG_GRID) return 0;
+  const int gx = c / COG_GRID, gy = c - gx * COG_GRID;
+  if (gx >= eg.dimx || gy >= eg.dimy) return 0;
+  return grid_at(g, gx - 1 + eg.minx, gy - 1 + eg.miny);
+}
+
+// 16 output bytes [16j, 16j+16) of the 16,128-byte map block
+DEV uint4 encode_chunk(const uint8_t *g, const EncGeom &eg, int j) {
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
+  const int b0 = 16 * j;
+  int c = b0 / 7;
+  int f = b0 - 7 * c;
+  uint8_t code = cell_code(g, eg, c);
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    w[k >> 2] |= feat_byte(code, f) << (8 * (k & 3));
+    if (++f == 7) {
+      f = 0;
+      ++c;
+      code = cell_code(g, eg, c);
+    }
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+DEV void encode_env(const DevState &s, size_t env, int t, int nt) {
+  const EnvPriv *pv = s.priv + env;
+  EncGeom eg{pv->minx, pv->miny, pv->dimx, pv->dimy};
+  const uint8_t *g = s.grid + env * (size_t)kGridBytes;
+  uint4 *out = reinterpret_cast<uint4 *>(s.obs + env * COG_OBS_BYTES);
+  for (int j = t; j < COG_OBS_MAP_BYTES / 16; j += nt) out[j] = encode_chunk(g, eg, j);
+}
+
+// the wave encodes, one after another, every env of its 64 that was (re)generated
+DEV void wave_encode(const DevState &s, size_t i, bool enc) {
+  uint64_t m = __ballot(enc);
+  const int lane = threadIdx.x & 63;
+  while (m) {
+    const int l = __ffsll((unsigned long long)m) - 1;
+    m &= m - 1;
+    const size_t env = (size_t)__shfl((int)i, l);
+    encode_env(s, env, lane, 64);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// sampler (sampler.h:14-79): 5 independent uniform picks over the set bits of each head
+// ------------------------------------------------------------------------------------------
+DEV uint32_t bools4(uint32_t w) {                          // 4 bool bytes -> 4 bits (nonzero = set)
+  const uint32_t nz = (((w & 0x7f7f7f7fu) + 0x7f7f7f7fu) | w) & 0x80808080u;
+  return ((nz >> 7) * 0x01020408u) >> 24 & 0xfu;
+}
+DEV uint32_t nth_set_bit(uint32_t m, uint32_t j) {        // index of the j-th (0-based) set bit
+  uint32_t base = 0;
+  uint32_t c = __popc(m & 0xffffu);
+  if (j >= c) { j -= c; base += 16; m >>= 16; }
+  c = __popc(m & 0xffu);
+  if (j >= c) { j -= c; base += 8; m >>= 8; }
+  c = __popc(m & 0xfu);
+  if (j >= c) { j -= c; base += 4; m >>= 4; }
+  c = __popc(m & 0x3u);
+  if (j >= c) { j -= c; base += 2; m >>= 2; }
+  c = m & 1u;
+  if (j >= c) { base += 1; }
+  return base;
+}
+DEV uint8_t pick(uint32_t &rng, uint32_t m) {
+  const uint32_t k = __popc(m);
+  if (!k) return 0;
+  return (uint8_t)nth_set_bit(m, uid(rng, k));
+}
+DEV void sample_mask(const uint8_t *mask, uint32_t &rng, uint8_t out[5]) {
+  const uint4 *m4 = reinterpret_cast<const uint4 *>(mask);
+  uint64_t lo = 0, hi = 0;
+#pragma unroll
+  for (int q = 0; q < 6; q++) {
+    const uint4 v = m4[q];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int word = 4 * q + k;                          // bytes 4*word .. 4*word+3
+      if (word >= 23) break;
+      const uint64_t b = bools4(w[k]);
+      const int bit = 4 * word;
+      if (bit < 64) lo |= b << bit;
+      else hi |= b << (bit - 64);
+    }
+  }
+  const uint32_t play = (uint32_t)(lo & 0x3fffffu);
+  const uint32_t spec = (uint32_t)((lo >> 22) & 0x3fffffu);
+  const uint32_t rem = (uint32_t)(((lo >> 44) | (hi << 20)) & 0x3fffffu);
+  const uint32_t mov = (uint32_t)((hi >> 2) & 0x7fu);
+  const uint32_t shop = (uint32_t)((hi >> 9) & 0x7ffffu);
+  out[0] = pick(rng, play);
+  out[1] = pick(rng, spec);
+  out[2] = pick(rng, rem);
+  out[3] = pick(rng, mov);
+  out[4] = pick(rng, shop);
+}
+DEV void store_action(uint8_t *dst, const uint8_t a[5]) {
+  const uint32_t lo = (uint32_t)a[0] | (uint32_t)a[1] << 8 | (uint32_t)a[2] << 16 | (uint32_t)a[3] << 24;
+  reinterpret_cast<uint2 *>(dst)[0] = make_uint2(lo, (uint32_t)a[4]);
+}
+
+// ------------------------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------------------------
+__global__ void k_init(DevState s, uint32_t default_seed) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= s.n) return;
+  EnvPriv *pv = s.priv + i;
+  EnvPriv z;
+  memset(&z, 0, sizeof(z));
+  z.seed = default_seed + (uint32_t)i;
+  z.rng = mr_seed(z.seed);
+  z.n_players = 4; z.n_pieces = 3; z.difficulty = 0; z.max_steps = 100000;
+  z.n_in_market = COG_MKT_SLOTS;
+  z.in_market = kInMarket0;
+  *pv = z;
+  uint8_t *ob = s.obs + i * COG_OBS_BYTES;
+  for (int k = 0; k < COG_N_SHOP; k++) ob[COG_OBS_SHOP + k] = COG_CARDS_PER_TYPE;
+  uint8_t *sel = s.sel + i * COG_MASK_BYTES;
+  for (int m = 0; m < 5; m++) {                            // ActionMask() defaults (Q26)
+    uint8_t *am = m == 4 ? sel : ob + COG_OBS_PLAYER0 + COG_OBS_PLAYER_STRIDE * m + COG_PD_MASK;
+    am[COG_MASK_PLAY] = am[COG_MASK_SPECIAL] = am[COG_MASK_REMOVE] = 1;
+    am[COG_MASK_MOVE] = am[COG_MASK_SHOP] = 1;
+  }
+}
+
+__global__ void k_reset(DevState s, ResetParams p) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= s.n) return;
+  Ctx e = make_ctx(s, i);
+  EnvPriv *pv = e.pv;
+  if (p.use_params) {                                      // cog_env::reset(params) :66-77
+    pv->n_players = p.n_players;
+    pv->n_pieces = p.n_pieces;
+    pv->difficulty = p.difficulty;
+    pv->max_steps = p.max_steps;
+    pv->seed = p.seed + (uint32_t)i;                       // vec_environment.h:41, u32 wrap (Q33)
+    pv->rng = mr_seed(pv->seed);
+  }
+  if (!env_reset(e)) {
+    atomicOr(&s.status[0], pv->flags);
+    atomicAdd(&s.status[1], 1u);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_encode(DevState s) {
+  const size_t env = blockIdx.x;
+  if (env >= s.n) return;
+  EnvPriv *pv = s.priv + env;
+  if (!pv->need_encode) return;
+  encode_env(s, env, threadIdx.x, blockDim.x);
+  __syncthreads();
+  if (threadIdx.x == 0) pv->need_encode = 0;
+}
+
+DEV void step_one(const DevState &s, size_t i, const uint8_t *act, bool &enc) {
+  Ctx e = make_ctx(s, i);
+  env_step(e, act);
+  EnvPriv *pv = e.pv;
+  s.done[i] = pv->done;
+  if (pv->done) {                                          // vec_environment.h:56-59
+    if (!env_reset(e)) {
+      atomicOr(&s.status[0], pv->flags);
+      atomicAdd(&s.status[1], 1u);
+    } else {
+      enc = true;
+      pv->need_encode = 0;
+      const uint32_t k = atomicAdd(&s.status[2], 1u);
+      if (k < s.n) s.dirty[k] = (uint32_t)i;
+    }
+  }
+  s.agent[i] = pv->agent;
+}
+
+__global__ void __launch_bounds__(256) k_step(DevState s, const uint8_t *__restrict__ actions) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool enc = false;
+  if (i < s.n) step_one(s, i, actions + i * COG_ACTION_BYTES, enc);
+  wave_encode(s, i, enc);
+}
+
+__global__ void __launch_bounds__(256) k_sample(size_t n, const uint8_t *__restrict__ masks,
+                                                uint32_t *__restrict__ rngs, uint8_t *__restrict__ actions) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t rng = rngs[i];
+  uint8_t a[5];
+  sample_mask(masks + i * COG_MASK_BYTES, rng, a);
+  rngs[i] = rng;
+  store_action(actions + i * COG_ACTION_BYTES, a);
+}
+
+__global__ void __launch_bounds__(256) k_sample_step(DevState s, int mask_source, uint32_t *__restrict__ rngs,
+                                                     uint8_t *__restrict__ actions) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool enc = false;
+  if (i < s.n) {
+    const uint8_t *mask = mask_source == MASK_STORED
+        ? s.obs + i * COG_OBS_BYTES + COG_OBS_PLAYER0 + COG_OBS_PLAYER_STRIDE * s.priv[i].agent + COG_PD_MASK
+        : s.sel + i * COG_MASK_BYTES;
+    uint32_t rng = rngs[i];
+    uint8_t a[5];
+    sample_mask(mask, rng, a);
+    rngs[i] = rng;
+    uint8_t *ad = actions + i * COG_ACTION_BYTES;
+    store_action(ad, a);
+    const uint8_t act[5] = {a[0], a[1], a[2], a[3], a[4]};
+    step_one(s, i, act, enc);
+  }
+  wave_encode(s, i, enc);
+}
+
+__global__ void k_seed_sampler(size_t n, uint32_t seed, uint32_t *rngs) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) rngs[i] = mr_seed((uint64_t)seed + (uint64_t)i);   // vec_sampler.h:9-13 (no u32 wrap)
+}
+
+// ------------------------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------------------------
+static inline unsigned blocks_for(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
+int launch_init(const DevState &s, const uint32_t *, uint32_t default_seed, void *stream) {
+  if (!s.n) return 0;
+  hipLaunchKernelGGL(k_init, dim3(blocks_for(s.n, 256)), dim3(256), 0, (hipStream_t)stream, s, default_seed);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int launch_reset(const DevState &s, const ResetParams &p, void *stream) {
+  if (!s.n) return 0;
+  hipLaunchKernelGGL(k_reset, dim3(blocks_for(s.n, 64)), dim3(64), 0, (hipStream_t)stream, s, p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int launch_encode_all(const DevState &s, void *stream) {
+  if (!s.n) return 0;
+  hipLaunchKernelGGL(k_encode, dim3((unsigned)s.n), dim3(256), 0, (hipStream_t)stream, s);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int launch_step(const DevState &s, const uint8_t *d_actions, void *stream) {
+  if (!s.n) return 0;
+  hipLaunchKernelGGL(k_step, dim3(blocks_for(s.n, 256)), dim3(256), 0, (hipStream_t)stream, s, d_actions);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int launch_sample(size_t n, const uint8_t *d_masks, uint32_t *d_rng, uint8_t *d_actions, void *stream) {
+  if (!n) return 0;
+  hipLaunchKernelGGL(k_sample, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, n, d_masks, d_rng, d_actions);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int launch_sample_step(const DevState &s, int mask_source, uint32_t *d_rng, uint8_t *d_actions, void *stream) {
+  if (!s.n) return 0;
+  hipLaunchKernelGGL(k_sample_step, dim3(blocks_for(s.n, 256)), dim3(256), 0, (hipStream_t)stream, s,
+                     mask_source, d_rng, d_actions);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int launch_seed_sampler(size_t n, uint32_t seed, uint32_t *d_rng, void *stream) {
+  if (!n) return 0;
+  hipLaunchKernelGGL(k_seed_sampler, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, n, seed, d_rng);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace cog

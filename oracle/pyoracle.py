@@ -17,17 +17,17 @@ ORACLE_SO = os.path.join(HERE, "liboracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libref.so")
 
 # ---- numpy records mirroring reference include/api.h:67-161 (field order as registered by
-# ---- PYBIND11_NUMPY_DTYPE at src/pybind/common.cpp:8-20) ---------------------------------
+# ---- PYBIND11_NUMPY_DTYPE at src/pybind/common.cpp:8-20; pybind11 orders fields by offset) -
 DECK = np.dtype({"names": ["draw", "hand", "active", "played", "discard"],
                  "formats": [("u1", (21,))] * 5, "offsets": [0, 21, 42, 63, 84], "itemsize": 105})
-MASK = np.dtype({"names": ["play", "play_special", "remove", "get_from_shop", "move"],
-                 "formats": [("?", (22,)), ("?", (22,)), ("?", (22,)), ("?", (19,)), ("?", (7,))],
-                 "offsets": [0, 22, 44, 73, 66], "itemsize": 128})
+MASK = np.dtype({"names": ["play", "play_special", "remove", "move", "get_from_shop"],
+                 "formats": [("?", (22,)), ("?", (22,)), ("?", (22,)), ("?", (7,)), ("?", (19,))],
+                 "offsets": [0, 22, 44, 66, 73], "itemsize": 128})
 PLAYER = np.dtype({"names": ["obs", "action_mask"], "formats": [DECK, MASK],
                    "offsets": [0, 128], "itemsize": 256})
-SHARED = np.dtype({"names": ["map", "phase", "shop", "current_resources"],
-                   "formats": [("u1", (48, 48, 7)), "u1", ("u1", (18,)), ("<f4", (3,))],
-                   "offsets": [0, 16128, 16144, 16132], "itemsize": 16164})
+SHARED = np.dtype({"names": ["map", "phase", "current_resources", "shop"],
+                   "formats": [("u1", (48, 48, 7)), "u1", ("<f4", (3,)), ("u1", (18,))],
+                   "offsets": [0, 16128, 16132, 16144], "itemsize": 16164})
 OBS = np.dtype({"names": ["shared", "player_data"], "formats": [SHARED, (PLAYER, (4,))],
                 "offsets": [0, 16192], "itemsize": 17216})
 ACTION = np.dtype({"names": ["play", "play_special", "remove", "move", "get_from_shop"],
