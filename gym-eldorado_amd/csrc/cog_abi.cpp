@@ -380,6 +380,27 @@ int cog_env_clear_hazards(cog_env *env) {
   return COG_OK;
 }
 
+int cog_env_time_encode(cog_env *env, int iters, double *ms_per_launch) {
+  if (!env || iters < 1 || !ms_per_launch) return fail(COG_ERR_INVALID, "bad argument");
+  DeviceGuard g(env->device);
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  if (cog::launch_encode_all(env->s, env->stream, 1))   // warm-up launch
+    return fail(COG_ERR_HIP, "encode launch failed");
+  HIPCHK(hipEventRecord(e0, env->stream));
+  for (int k = 0; k < iters; k++)
+    if (cog::launch_encode_all(env->s, env->stream, 1)) return fail(COG_ERR_HIP, "encode launch failed");
+  HIPCHK(hipEventRecord(e1, env->stream));
+  HIPCHK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  *ms_per_launch = (double)ms / iters;
+  return COG_OK;
+}
+
 void *cog_env_stream(cog_env *env) { return env ? (void *)env->stream : nullptr; }
 int cog_env_device(const cog_env *env) { return env ? env->device : -1; }
 

@@ -99,7 +99,7 @@ enum MaskSource : int { MASK_SELECTED = 0, MASK_STORED = 1, MASK_EXTERNAL = 2 };
 int launch_init(const DevState &s, const uint32_t *seeds_host_unused, uint32_t default_seed,
                 void *stream);
 int launch_reset(const DevState &s, const ResetParams &p, void *stream);
-int launch_encode_all(const DevState &s, void *stream);
+int launch_encode_all(const DevState &s, void *stream, int force = 0);
 int launch_step(const DevState &s, const uint8_t *d_actions, void *stream);
 int launch_sample(size_t n, const uint8_t *d_masks, uint32_t *d_rng, uint8_t *d_actions,
                   void *stream);

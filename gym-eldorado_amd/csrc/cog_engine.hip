@@ -957,11 +957,11 @@ __global__ void k_reset(DevState s, ResetParams p) {
   }
 }
 
-__global__ void __launch_bounds__(256) k_encode(DevState s) {
+__global__ void __launch_bounds__(256) k_encode(DevState s, int force) {
   const size_t env = blockIdx.x;
   if (env >= s.n) return;
   EnvPriv *pv = s.priv + env;
-  if (!pv->need_encode) return;
+  if (!force && !pv->need_encode) return;
   encode_env(s, env, threadIdx.x, blockDim.x);
   __syncthreads();
   if (threadIdx.x == 0) pv->need_encode = 0;
@@ -1044,9 +1044,9 @@ int launch_reset(const DevState &s, const ResetParams &p, void *stream) {
   hipLaunchKernelGGL(k_reset, dim3(blocks_for(s.n, 64)), dim3(64), 0, (hipStream_t)stream, s, p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-int launch_encode_all(const DevState &s, void *stream) {
+int launch_encode_all(const DevState &s, void *stream, int force) {
   if (!s.n) return 0;
-  hipLaunchKernelGGL(k_encode, dim3((unsigned)s.n), dim3(256), 0, (hipStream_t)stream, s);
+  hipLaunchKernelGGL(k_encode, dim3((unsigned)s.n), dim3(256), 0, (hipStream_t)stream, s, force);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_step(const DevState &s, const uint8_t *d_actions, void *stream) {

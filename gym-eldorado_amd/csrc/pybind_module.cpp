@@ -271,7 +271,12 @@ PYBIND11_MODULE(_city_of_gold, m) {
         return py::make_tuple(acc, per);
       })
       .def("clear_hazards", [](VecEnv &e) { check(cog_env_clear_hazards(e.handle())); })
-      .def("sync_host", [](VecEnv &e) { check(cog_env_sync_host(e.handle())); });
+      .def("sync_host", [](VecEnv &e) { check(cog_env_sync_host(e.handle())); })
+      .def("time_encode", [](VecEnv &e, int iters) {
+        double ms = 0;
+        check(cog_env_time_encode(e.handle(), iters, &ms));
+        return ms;
+      }, "iters"_a = 20);
 
   py::class_<VecSampler>(m, "VecSamplerBase", py::dynamic_attr())
       .def(py::init<size_t, std::optional<size_t>, std::optional<int>>(), "n_envs"_a, "seed"_a = py::none(),
