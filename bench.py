@@ -67,7 +67,8 @@ class Dist:
             import torch
             import torch.distributed as dist
             self.torch = torch
-            torch.cuda.set_device(self.local)
+            if torch.cuda.is_available():
+                torch.cuda.set_device(self.local)
             dist.init_process_group("gloo")      # timing barrier / max only: no data-path collective
             self.dist = dist
             self.pg = True
@@ -81,7 +82,7 @@ class Dist:
 
     def barrier_sync(self, runner):
         runner.sync()
-        if self.torch is not None:
+        if self.torch is not None and self.torch.cuda.is_available():
             self.torch.cuda.synchronize()
         if self.pg:
             self.dist.barrier()

@@ -11,14 +11,28 @@
 #include "vec_environment.h"
 #include "vec_sampler.h"
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
+#include <new>
 
 using env1 = vec_cog_env<1>;
 using smp1 = vec_action_sampler<1>;
 
+// Constructed in zero-filled memory: the reference leaves Player::has_won of players >=
+// n_players uninitialised (player.cpp:45) and sums it into every reward (environment.cpp:
+// 283-285).  Zeroed storage is the state of fresh pages and the behaviour the
+// engine defines; heap reuse would otherwise make 2/3-player rewards depend on process history.
 extern "C" {
-void *ref_create() { return new env1(); }
-void ref_destroy(void *h) { delete static_cast<env1 *>(h); }
+void *ref_create() {
+  const size_t bytes = (sizeof(env1) + 63) / 64 * 64;
+  void *mem = std::aligned_alloc(64, bytes);
+  std::memset(mem, 0, bytes);
+  return new (mem) env1();
+}
+void ref_destroy(void *h) {
+  static_cast<env1 *>(h)->~env1();
+  std::free(h);
+}
 int ref_reset(void *h, uint32_t seed, uint8_t np, uint8_t npieces, int diff, uint32_t max_steps) {
   try {
     static_cast<env1 *>(h)->reset(seed, np, npieces, static_cast<Difficulty>(diff), max_steps, false);

@@ -1,0 +1,84 @@
+"""CPU, world_size 2 over gloo: the multi-GPU path shards envs by index with no data-path
+collective.  Each rank steps its shard (C oracle standing in for its GPU) with global-index
+seeds; the gathered per-env digests must equal a single-process run of the whole batch.
+Also exercises bench.py's timing barrier / max / sum helpers."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+N_TOTAL, STEPS, SEED = 20, 120, 4242
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def digests(vec, smp, lo, hi):
+    import pyoracle as po
+    return [po.step_digest(vec.observations[i:i + 1], vec.selected_action_masks[i:i + 1],
+                           vec.rewards[i:i + 1], vec.dones[i:i + 1], vec.agent_selection[i:i + 1],
+                           vec.infos[i:i + 1], smp.actions[i:i + 1]) for i in range(lo, hi)]
+
+
+def rollout(n, seed, steps):
+    import pyoracle as po
+    vec, smp = po.OracleVec(n), po.OracleSampler(n, seed)
+    vec.reset(seed, 4, 3, 2, 30)
+    for _ in range(steps):
+        smp.sample(po.stored_masks(vec))
+        vec.step(smp.actions)
+    return digests(vec, smp, 0, n)
+
+
+def worker(rank, world, port, root, q):
+    import sys
+    for p in (os.path.join(root, "gym-eldorado_amd"), os.path.join(root, "oracle"), root):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import bench
+    from city_of_gold.shard import shard, shard_seed
+    d = bench.Dist(world)
+    lo, hi = shard(N_TOTAL, rank, world)
+    mine = rollout(hi - lo, shard_seed(SEED, lo), STEPS)
+    gathered = [None] * world
+    d.dist.all_gather_object(gathered, (lo, [x.hex() for x in mine]))
+    mx = d.max(float(rank + 1))
+    tot = d.sum(float(hi - lo))
+    if rank == 0:
+        q.put((gathered, mx, tot))
+    d.close()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_shards_equal_single_process():
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, 2, port, root, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    gathered, mx, tot = q.get(timeout=240)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert mx == 2.0 and tot == N_TOTAL
+    full = [x.hex() for x in rollout(N_TOTAL, SEED, STEPS)]
+    merged = []
+    for lo, ds in sorted(gathered):
+        merged.extend(ds)
+    assert merged == full
+
+
+def test_shard_blocks():
+    from city_of_gold.shard import shard
+    assert [shard(10, r, 3) for r in range(3)] == [(0, 3), (3, 6), (6, 10)]
+    assert sum(h - l for l, h in (shard(65536 * 8, r, 8) for r in range(8))) == 65536 * 8
