@@ -114,7 +114,7 @@ void env_free(cog_env *e) {
   DeviceGuard g(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   void *dev[] = {e->s.obs, e->s.sel, e->s.info, e->s.rew, e->s.done, e->s.agent, e->s.priv,
-                 e->s.grid, e->s.gen, e->s.status, e->s.dirty, e->d_actions};
+                 e->s.grid, e->s.cgrid, e->s.gen, e->s.status, e->s.dirty, e->d_actions};
   for (void *p : dev)
     if (p) (void)hipFree(p);
   void *hst[] = {e->h_obs, e->h_sel, e->h_rew, e->h_done, e->h_agent, e->h_info, e->h_status};
@@ -239,7 +239,7 @@ int cog_env_create(size_t n_envs, int device, cog_env **out) {
       (rc = dmalloc(&s.info, n * COG_INFO_BYTES)) || (rc = dmalloc(&s.rew, n * 4 * sizeof(float))) ||
       (rc = dmalloc(&s.done, n)) || (rc = dmalloc(&s.agent, n)) ||
       (rc = dmalloc(&s.priv, n * sizeof(cog::EnvPriv))) ||
-      (rc = dmalloc(&s.grid, n * (size_t)cog::kGridBytes)) ||
+      (rc = dmalloc(&s.grid, n * (size_t)cog::kGridBytes)) || (rc = dmalloc(&s.cgrid, n * (size_t)COG_CELLS)) ||
       (rc = dmalloc(&s.gen, n * sizeof(cog::GenScratch))) || (rc = dmalloc(&s.status, 64)) ||
       (rc = dmalloc(&s.dirty, n * sizeof(uint32_t))) || (rc = dmalloc(&e->d_actions, n * COG_ACTION_BYTES)) ||
       (rc = hmalloc(&e->h_status, 64))) {
@@ -249,6 +249,7 @@ int cog_env_create(size_t n_envs, int device, cog_env **out) {
   struct { void *p; size_t b; } z[] = {
       {s.obs, n * COG_OBS_BYTES}, {s.sel, n * COG_MASK_BYTES}, {s.info, n * COG_INFO_BYTES},
       {s.rew, n * 4 * sizeof(float)}, {s.done, n}, {s.agent, n}, {s.grid, n * (size_t)cog::kGridBytes},
+      {s.cgrid, n * (size_t)COG_CELLS},
       {s.gen, n * sizeof(cog::GenScratch)}, {s.status, 64}, {e->d_actions, n * COG_ACTION_BYTES}};
   for (auto &zz : z)
     if (zz.b && hipMemsetAsync(zz.p, 0, zz.b, e->stream) != hipSuccess) {
@@ -380,17 +381,17 @@ int cog_env_clear_hazards(cog_env *env) {
   return COG_OK;
 }
 
-int cog_env_time_encode(cog_env *env, int iters, double *ms_per_launch) {
+int cog_env_time_encode(cog_env *env, int iters, int variant, double *ms_per_launch) {
   if (!env || iters < 1 || !ms_per_launch) return fail(COG_ERR_INVALID, "bad argument");
   DeviceGuard g(env->device);
   hipEvent_t e0, e1;
   HIPCHK(hipEventCreate(&e0));
   HIPCHK(hipEventCreate(&e1));
-  if (cog::launch_encode_all(env->s, env->stream, 1))   // warm-up launch
+  if (cog::launch_encode_all(env->s, env->stream, variant))   // warm-up launch
     return fail(COG_ERR_HIP, "encode launch failed");
   HIPCHK(hipEventRecord(e0, env->stream));
   for (int k = 0; k < iters; k++)
-    if (cog::launch_encode_all(env->s, env->stream, 1)) return fail(COG_ERR_HIP, "encode launch failed");
+    if (cog::launch_encode_all(env->s, env->stream, variant)) return fail(COG_ERR_HIP, "encode launch failed");
   HIPCHK(hipEventRecord(e1, env->stream));
   HIPCHK(hipEventSynchronize(e1));
   float ms = 0.f;

@@ -14,6 +14,9 @@
 //   grid  [N] x 16384 B   absolute-coordinate hex-code grid, 128 x 128 cells, cell (x, y) at
 //                         (x + 64) * 128 + (y + 64); 0 = no hex.  Built by map generation,
 //                         read by movement masks, done checks and the map-observation encode.
+//   cgrid [N] x 2304 B    compact 48x48 hex-code grid of the final map in observation cell order
+//                         (the lookup table of movement masks / done checks, and the source of
+//                         the map-observation encode)
 //   gen   [N] x 256 B     map-generation scratch (pieces list, per-env piece transforms)
 #pragma once
 #include <stddef.h>
@@ -26,6 +29,7 @@ namespace cog {
 constexpr int kGridDim = 128;
 constexpr int kGridOff = 64;
 constexpr int kGridBytes = kGridDim * kGridDim;
+#define COG_CELLS 2304                // 48 * 48
 constexpr int kMaxCoord = 62;        // |x|,|y| of any placed hex; beyond -> hazard GRID_OVER
 constexpr int kMaxPlaced = 96;       // pieces placed in one generation (incl. recursion)
 
@@ -57,7 +61,7 @@ struct alignas(64) EnvPriv {         // cog_env private members (environment.h:1
   uint32_t in_market;                // Shop::in_market bits
   uint32_t flags;                    // sticky hazard flags
   int8_t minx, miny, maxx, maxy;     // Map::min_xy / max_xy (integer hex coords)
-  uint8_t dimx, dimy, need_encode, pad0;
+  uint8_t dimx, dimy, pad0, pad1b;
   int8_t locx[4], locy[4];           // Map::player_locations
   uint32_t pad1[4];
   PlayerPriv pl[4];
@@ -82,6 +86,7 @@ struct DevState {
   uint8_t *agent;
   EnvPriv *priv;
   uint8_t *grid;
+  uint8_t *cgrid;                    // [n] x 2304 B compact 48x48 hex codes (lookups + encode)
   GenScratch *gen;
   uint32_t *status;                  // [0] OR of error flags, [1] error count, [2] dirty count
   uint32_t *dirty;                   // [n] envs whose map was re-generated (host view refresh)
@@ -99,7 +104,7 @@ enum MaskSource : int { MASK_SELECTED = 0, MASK_STORED = 1, MASK_EXTERNAL = 2 };
 int launch_init(const DevState &s, const uint32_t *seeds_host_unused, uint32_t default_seed,
                 void *stream);
 int launch_reset(const DevState &s, const ResetParams &p, void *stream);
-int launch_encode_all(const DevState &s, void *stream, int force = 0);
+int launch_encode_all(const DevState &s, void *stream, int variant = 0);
 int launch_step(const DevState &s, const uint8_t *d_actions, void *stream);
 int launch_sample(size_t n, const uint8_t *d_masks, uint32_t *d_rng, uint8_t *d_actions,
                   void *stream);

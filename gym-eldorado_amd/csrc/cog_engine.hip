@@ -14,7 +14,7 @@
 // Kernels:
 //   k_init           default-construct N envs (vec_environment.h:23-30)
 //   k_reset          cog_env::reset(params) incl. procedural map generation (map.cpp:697-742)
-//   k_encode         48x48x7 map-observation encode (map.cpp:389-405): streaming, 1 WG / env
+//   k_encode         48x48x7 map-observation encode (map.cpp:389-405): streaming, 16 cells / item
 //   k_sample         masked uniform sampler (sampler.h:14-79)
 //   k_step           vec_cog_env::step with auto-reset (vec_environment.h:46-61)
 //   k_sample_step    runner-fused sample(selected|stored masks) + step (runner.h:46-55)
@@ -80,7 +80,8 @@ struct Ctx {
   uint8_t *info;      // Info record
   float *rew;         // rewards[4]
   EnvPriv *pv;        // private state
-  uint8_t *grid;      // 128x128 hex codes
+  uint8_t *grid;      // 128x128 absolute hex codes (map-generation scratch)
+  uint8_t *cgrid;     // 48x48 compact hex codes of the final map
   GenScratch *gs;
 };
 
@@ -92,9 +93,12 @@ DEV Ctx make_ctx(const DevState &s, size_t i) {
   e.rew = s.rew + i * 4;
   e.pv = s.priv + i;
   e.grid = s.grid + i * (size_t)kGridBytes;
+  e.cgrid = s.cgrid + i * COG_CELLS;
   e.gs = s.gen + i;
   return e;
 }
+
+DEV void build_cgrid(const Ctx &e);
 
 DEV uint8_t *deck(const Ctx &e, int p) { return e.ob + COG_OBS_PLAYER0 + COG_OBS_PLAYER_STRIDE * p; }
 DEV uint8_t *stm(const Ctx &e, int p) { return deck(e, p) + COG_PD_MASK; }
@@ -111,7 +115,8 @@ DEV uint8_t lookup(const Ctx &e, int x, int y) {
     pv->flags |= F_OOB_LOOKUP;
     return COG_HEX_MOUNTAIN;
   }
-  const uint8_t c = grid_at(e.grid, x, y);
+  if (ix >= COG_GRID || iy >= COG_GRID) return COG_HEX_MOUNTAIN;   // ring cell of a 49-wide map
+  const uint8_t c = e.cgrid[ix * COG_GRID + iy];
   return c ? c : (uint8_t)COG_HEX_MOUNTAIN;
 }
 
@@ -675,6 +680,7 @@ DEV bool env_reset(const Ctx &e) {
     pv->flags |= F_MAPGEN_FAIL;
     return false;
   }
+  build_cgrid(e);
   for (int i = 0; i < pv->n_players; i++) player_reset(e, i);
   add_players(e);
   for (int k = 0; k < COG_N_SHOP; k++) e.ob[COG_OBS_SHOP + k] = COG_CARDS_PER_TYPE;
@@ -683,7 +689,6 @@ DEV bool env_reset(const Ctx &e) {
   pv->turn_counter = 0;
   for (int i = 0; i < pv->n_players; i++) update_observation(e, i);
   copy_mask(e.sel, stm(e, 0));
-  pv->need_encode = 1;
   return true;
 }
 
@@ -797,49 +802,54 @@ DEV void env_step(const Ctx &e, const uint8_t *act) {
 // ------------------------------------------------------------------------------------------
 // map-observation encode (map.cpp:389-405): feature 0 stays 0 (Q2), f[req+1] = n, f[6] = is_end
 // ------------------------------------------------------------------------------------------
-DEV uint32_t feat_byte(uint8_t code, int f) {
-  if (!code || f == 0) return 0;
-  if (f == 6) return COG_HEX_END(code);
-  const int req = COG_HEX_REQ(code);
-  return (req != COG_REQ_NULL && f == req + 1) ? COG_HEX_N(code) : 0u;
+// Feature f of a hex code, f known at compile time after unrolling.  Code 0 (no hex) and NULL
+// hexes (mountain / start, requirement 5) give all-zero features, like finalize's zero fill.
+DEV uint32_t feat(uint32_t code, int f) {
+  if (f == 0) return 0u;                                   // occupying player: never written (Q2)
+  if (f == 6) return (code >> 6) & 1u;                     // is_end
+  return (((code >> 3) & 7u) == (uint32_t)(f - 1)) ? (code & 7u) : 0u;
 }
 
-struct EncGeom {
-  int minx, miny, dimx, dimy;
-};
-
-DEV uint8_t cell_code(const uint8_t *g, const EncGeom &eg, int c) {
-  if (c >= COG_GRID * COG_GRID) return 0;
-  const int gx = c / COG_GRID, gy = c - gx * COG_GRID;
-  if (gx >= eg.dimx || gy >= eg.dimy) return 0;
-  return grid_at(g, gx - 1 + eg.minx, gy - 1 + eg.miny);
-}
-
-// 16 output bytes [16j, 16j+16) of the 16,128-byte map block
-DEV uint4 encode_chunk(const uint8_t *g, const EncGeom &eg, int j) {
-  uint32_t w[4] = {0u, 0u, 0u, 0u};
-  const int b0 = 16 * j;
-  int c = b0 / 7;
-  int f = b0 - 7 * c;
-  uint8_t code = cell_code(g, eg, c);
+// One 16-cell block k (cells 16k..16k+15 of the 48x48 grid, row-major [ix][iy] like the
+// observation) -> output bytes [112k, 112k+112) of the 16,128-byte map: one aligned 16-byte
+// load of hex codes, seven aligned 16-byte stores.  The byte -> (cell, feature) map is static.
+DEV void encode_block(const uint8_t *__restrict__ cgrid, uint8_t *__restrict__ map, int k) {
+  const uint4 c4 = reinterpret_cast<const uint4 *>(cgrid)[k];
+  const uint32_t cw[4] = {c4.x, c4.y, c4.z, c4.w};
+  uint32_t w[28];
 #pragma unroll
-  for (int k = 0; k < 16; k++) {
-    w[k >> 2] |= feat_byte(code, f) << (8 * (k & 3));
-    if (++f == 7) {
-      f = 0;
-      ++c;
-      code = cell_code(g, eg, c);
-    }
+  for (int q = 0; q < 28; q++) w[q] = 0u;
+#pragma unroll
+  for (int b = 0; b < 112; b++) {
+    const int c = b / 7, f = b % 7;
+    const uint32_t code = (cw[c >> 2] >> (8 * (c & 3))) & 0xffu;
+    w[b >> 2] |= feat(code, f) << (8 * (b & 3));
   }
-  return make_uint4(w[0], w[1], w[2], w[3]);
+  uint4 *out = reinterpret_cast<uint4 *>(map + 112 * k);
+#pragma unroll
+  for (int q = 0; q < 7; q++) out[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
 
-DEV void encode_env(const DevState &s, size_t env, int t, int nt) {
-  const EnvPriv *pv = s.priv + env;
-  EncGeom eg{pv->minx, pv->miny, pv->dimx, pv->dimy};
-  const uint8_t *g = s.grid + env * (size_t)kGridBytes;
-  uint4 *out = reinterpret_cast<uint4 *>(s.obs + env * COG_OBS_BYTES);
-  for (int j = t; j < COG_OBS_MAP_BYTES / 16; j += nt) out[j] = encode_chunk(g, eg, j);
+constexpr int kEncBlocks = COG_GRID * COG_GRID / 16;     // 144 blocks per env
+
+// finalize's index mapping (map.cpp:335-340, 389-405): compact 48x48 code grid of the final
+// map, cell (ix, iy) = hex at (ix - 1 + min_x, iy - 1 + min_y) or 0.  Also the lookup table of
+// every movement mask / done check (hex_array, map.cpp:273-275).
+DEV void build_cgrid(const Ctx &e) {
+  const EnvPriv *pv = e.pv;
+  const int minx = pv->minx, miny = pv->miny, dx = pv->dimx, dy = pv->dimy;
+  uint4 *out = reinterpret_cast<uint4 *>(e.cgrid);
+  for (int k = 0; k < kEncBlocks; k++) {
+    const int ix = k / 3, iy0 = (k % 3) * 16;
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (ix < dx) {
+      const uint8_t *row = e.grid + (ix - 1 + minx + kGridOff) * kGridDim + kGridOff + miny - 1;
+#pragma unroll
+      for (int j = 0; j < 16; j++)
+        if (iy0 + j < dy) w[j >> 2] |= (uint32_t)row[iy0 + j] << (8 * (j & 3));
+    }
+    out[k] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
 }
 
 // the wave encodes, one after another, every env of its 64 that was (re)generated
@@ -850,7 +860,9 @@ DEV void wave_encode(const DevState &s, size_t i, bool enc) {
     const int l = __ffsll((unsigned long long)m) - 1;
     m &= m - 1;
     const size_t env = (size_t)__shfl((int)i, l);
-    encode_env(s, env, lane, 64);
+    const uint8_t *cg = s.cgrid + env * COG_CELLS;
+    uint8_t *map = s.obs + env * COG_OBS_BYTES;
+    for (int k = lane; k < kEncBlocks; k += 64) encode_block(cg, map, k);
   }
 }
 
@@ -957,14 +969,58 @@ __global__ void k_reset(DevState s, ResetParams p) {
   }
 }
 
-__global__ void __launch_bounds__(256) k_encode(DevState s, int force) {
-  const size_t env = blockIdx.x;
-  if (env >= s.n) return;
-  EnvPriv *pv = s.priv + env;
-  if (!force && !pv->need_encode) return;
-  encode_env(s, env, threadIdx.x, blockDim.x);
+// streaming map-observation encode over all envs: one work-item per 16-cell block
+__global__ void __launch_bounds__(256) k_encode_direct(const uint8_t *__restrict__ cgrid, uint8_t *__restrict__ obs,
+                                                       size_t n_blocks) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_blocks) return;
+  const size_t env = t / kEncBlocks;
+  const int k = (int)(t - env * kEncBlocks);
+  encode_block(cgrid + env * COG_CELLS, obs + env * COG_OBS_BYTES, k);
+}
+
+// Same work, transposed through LDS so every store wave-instruction writes 1 KiB contiguous:
+// item t builds its 112 bytes into LDS at 112*t (ds_write_b128, conflict-free at this stride),
+// then the workgroup streams the 256*112 bytes out as 16-byte chunks in address order.
+template <bool NT>
+__global__ void __launch_bounds__(256) k_encode_lds(const uint8_t *__restrict__ cgrid, uint8_t *__restrict__ obs,
+                                                    size_t n_blocks) {
+  __shared__ uint4 stage[256 * 7];
+  const size_t g0 = (size_t)blockIdx.x * 256;
+  const size_t t = g0 + threadIdx.x;
+  if (t < n_blocks) {
+    const size_t env = t / kEncBlocks;
+    const int k = (int)(t - env * kEncBlocks);
+    const uint4 c4 = reinterpret_cast<const uint4 *>(cgrid + env * COG_CELLS)[k];
+    const uint32_t cw[4] = {c4.x, c4.y, c4.z, c4.w};
+    uint32_t w[28];
+#pragma unroll
+    for (int q = 0; q < 28; q++) w[q] = 0u;
+#pragma unroll
+    for (int b = 0; b < 112; b++) {
+      const int c = b / 7, f = b % 7;
+      const uint32_t code = (cw[c >> 2] >> (8 * (c & 3))) & 0xffu;
+      w[b >> 2] |= feat(code, f) << (8 * (b & 3));
+    }
+#pragma unroll
+    for (int q = 0; q < 7; q++) stage[threadIdx.x * 7 + q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+  }
   __syncthreads();
-  if (threadIdx.x == 0) pv->need_encode = 0;
+  const size_t nb = n_blocks - g0 < 256 ? n_blocks - g0 : 256;
+  for (int j = threadIdx.x; j < (int)nb * 7; j += 256) {
+    const size_t gb = g0 + (size_t)(j / 7);
+    const size_t env = gb / kEncBlocks;
+    const int k = (int)(gb - env * kEncBlocks);
+    uint4 *dst = reinterpret_cast<uint4 *>(obs + env * COG_OBS_BYTES + 112 * k) + (j % 7);
+    if (NT) {
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      const uint4 v = stage[j];
+      u32x4 x = {v.x, v.y, v.z, v.w};
+      __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(dst));
+    } else {
+      *dst = stage[j];
+    }
+  }
 }
 
 DEV void step_one(const DevState &s, size_t i, const uint8_t *act, bool &enc) {
@@ -978,7 +1034,6 @@ DEV void step_one(const DevState &s, size_t i, const uint8_t *act, bool &enc) {
       atomicAdd(&s.status[1], 1u);
     } else {
       enc = true;
-      pv->need_encode = 0;
       const uint32_t k = atomicAdd(&s.status[2], 1u);
       if (k < s.n) s.dirty[k] = (uint32_t)i;
     }
@@ -1044,9 +1099,13 @@ int launch_reset(const DevState &s, const ResetParams &p, void *stream) {
   hipLaunchKernelGGL(k_reset, dim3(blocks_for(s.n, 64)), dim3(64), 0, (hipStream_t)stream, s, p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-int launch_encode_all(const DevState &s, void *stream, int force) {
+int launch_encode_all(const DevState &s, void *stream, int variant) {
   if (!s.n) return 0;
-  hipLaunchKernelGGL(k_encode, dim3((unsigned)s.n), dim3(256), 0, (hipStream_t)stream, s, force);
+  const size_t nb = s.n * kEncBlocks;
+  const dim3 g(blocks_for(nb, 256)), b(256);
+  if (variant == 1) hipLaunchKernelGGL(k_encode_lds<false>, g, b, 0, (hipStream_t)stream, s.cgrid, s.obs, nb);
+  else if (variant == 2) hipLaunchKernelGGL(k_encode_lds<true>, g, b, 0, (hipStream_t)stream, s.cgrid, s.obs, nb);
+  else hipLaunchKernelGGL(k_encode_direct, g, b, 0, (hipStream_t)stream, s.cgrid, s.obs, nb);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_step(const DevState &s, const uint8_t *d_actions, void *stream) {

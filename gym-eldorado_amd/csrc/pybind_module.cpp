@@ -272,11 +272,11 @@ PYBIND11_MODULE(_city_of_gold, m) {
       })
       .def("clear_hazards", [](VecEnv &e) { check(cog_env_clear_hazards(e.handle())); })
       .def("sync_host", [](VecEnv &e) { check(cog_env_sync_host(e.handle())); })
-      .def("time_encode", [](VecEnv &e, int iters) {
+      .def("time_encode", [](VecEnv &e, int iters, int variant) {
         double ms = 0;
-        check(cog_env_time_encode(e.handle(), iters, &ms));
+        check(cog_env_time_encode(e.handle(), iters, variant, &ms));
         return ms;
-      }, "iters"_a = 20);
+      }, "iters"_a = 20, "variant"_a = 0);
 
   py::class_<VecSampler>(m, "VecSamplerBase", py::dynamic_attr())
       .def(py::init<size_t, std::optional<size_t>, std::optional<int>>(), "n_envs"_a, "seed"_a = py::none(),

@@ -119,8 +119,9 @@ COG_API int cog_env_hazards(cog_env *env, uint32_t *flags_or, uint32_t *per_env)
 COG_API int cog_env_clear_hazards(cog_env *env);
 COG_API void *cog_env_stream(cog_env *env);     /* hipStream_t of the handle */
 /* diagnostics: re-run the map-observation encode (map.cpp:389-405) over all envs `iters`
- * times back to back; average device time per launch (HIP events).  Output is unchanged. */
-COG_API int cog_env_time_encode(cog_env *env, int iters, double *ms_per_launch);
+ * times back to back; average device time per launch (HIP events).  Output is unchanged.
+ * variant: 0 = production kernel, >0 = alternative implementations kept for A/B timing. */
+COG_API int cog_env_time_encode(cog_env *env, int iters, int variant, double *ms_per_launch);
 COG_API int cog_env_device(const cog_env *env); /* device ordinal */
 
 /* ---- masked uniform random sampler ------------------------------------------------------- */

@@ -79,3 +79,29 @@ void ref_sample(void *s, const void *mask) {
 }
 const void *ref_sampler_actions(void *s) { return static_cast<smp1 *>(s)->get_actions().data(); }
 }
+
+// Calibration only: the reference's own sequential loop (vec_cog_env<1>::step + action_sampler)
+// over n envs with the given (hazard-free) seeds, `steps` x (sample(selected mask); step).
+#include <chrono>
+#include <vector>
+extern "C" double ref_bench_seq(const uint32_t *seeds, int n, int steps, uint8_t np, uint8_t npieces, int diff) {
+  std::vector<env1 *> envs(n);
+  std::vector<smp1 *> smps(n);
+  for (int i = 0; i < n; i++) {
+    envs[i] = static_cast<env1 *>(ref_create());
+    envs[i]->reset(seeds[i], np, npieces, static_cast<Difficulty>(diff), 100000, false);
+    smps[i] = new smp1(seeds[i]);
+  }
+  auto t0 = std::chrono::steady_clock::now();
+  for (int t = 0; t < steps; t++)
+    for (int i = 0; i < n; i++) {
+      smps[i]->sample(envs[i]->get_selected_action_masks());
+      envs[i]->step(smps[i]->get_actions());
+    }
+  auto t1 = std::chrono::steady_clock::now();
+  for (int i = 0; i < n; i++) {
+    ref_destroy(envs[i]);
+    delete smps[i];
+  }
+  return std::chrono::duration<double>(t1 - t0).count();
+}
