@@ -51,7 +51,8 @@ struct PlayerPriv {                  // Player + Deck private members (player.h:
   uint32_t n_movements;
 };
 
-struct alignas(64) EnvPriv {         // cog_env private members (environment.h:12-33) + Map/Shop state
+struct EnvPriv {                    // cog_env private members (environment.h:12-33) + Map/Shop state
+                                     // (4-byte aligned: also lives in LDS step slots)
   uint32_t rng;                      // env minstd_rand0 state
   uint32_t seed;
   uint32_t max_steps;
@@ -90,6 +91,7 @@ struct DevState {
   GenScratch *gen;
   uint32_t *status;                  // [0] OR of error flags, [1] error count, [2] dirty count
   uint32_t *dirty;                   // [n] envs whose map was re-generated (host view refresh)
+  unsigned long long *stamps;        // diagnostic builds (COG_STAMPS) only: per-wave phase clocks
 };
 
 struct ResetParams {
