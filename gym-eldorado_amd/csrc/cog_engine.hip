@@ -726,6 +726,30 @@ DEV bool env_reset(const Ctx &e) {
   return true;
 }
 
+// done: Info + rewards (environment.cpp:187-207, get_reward :281-288)
+DEV void finish_episode(const Ctx &e) {
+  EnvPriv *pv = e.pv;
+  pv->done = 1;
+  *reinterpret_cast<uint32_t *>(e.info) = pv->turn_counter;
+  float n_winners = 0.f;
+  for (int q = 0; q < 4; q++) n_winners += (float)pv->pl[q].has_won;
+  for (int q = 0; q < pv->n_players; q++) {
+    const PlayerPriv &Q = pv->pl[q];
+    uint8_t *ai = e.info + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * q;
+    const float rw = (float)(pv->n_players * Q.has_won) - n_winners;
+    ai[0] = Q.steps_taken;
+    *reinterpret_cast<float *>(ai + 4) = rw;
+    *reinterpret_cast<uint32_t *>(ai + 8) = Q.n_movements;
+    ai[12] = Q.n_added_cards;
+    ai[13] = Q.n_added_cards;                          // get_n_removed (player.cpp:223-224)
+    *reinterpret_cast<uint32_t *>(ai + 16) = 0u;       // n_spent never incremented (Q14)
+    *reinterpret_cast<uint32_t *>(ai + 20) = 0u;
+    *reinterpret_cast<uint32_t *>(ai + 24) = 0u;
+    *reinterpret_cast<uint32_t *>(ai + 28) = Q.n_added_cards;
+    e.rew[q] = rw;
+  }
+}
+
 // cog_env::step (environment.cpp:91-224)
 DEV void env_step(const Ctx &e, const uint8_t *act) {
   EnvPriv *pv = e.pv;
@@ -809,27 +833,7 @@ DEV void env_step(const Ctx &e, const uint8_t *act) {
     apply_special(e, special, ag);
   } else {
     const uint8_t c = lookup(e, pv->locx[cur], pv->locy[cur]);
-    if (COG_HEX_END(c) || pv->turn_counter >= pv->max_steps) {
-      pv->done = 1;
-      *reinterpret_cast<uint32_t *>(e.info) = pv->turn_counter;
-      float n_winners = 0.f;
-      for (int q = 0; q < 4; q++) n_winners += (float)pv->pl[q].has_won;
-      for (int q = 0; q < pv->n_players; q++) {
-        const PlayerPriv &Q = pv->pl[q];
-        uint8_t *ai = e.info + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * q;
-        const float rw = (float)(pv->n_players * Q.has_won) - n_winners;
-        ai[0] = Q.steps_taken;
-        *reinterpret_cast<float *>(ai + 4) = rw;
-        *reinterpret_cast<uint32_t *>(ai + 8) = Q.n_movements;
-        ai[12] = Q.n_added_cards;
-        ai[13] = Q.n_added_cards;                          // get_n_removed (player.cpp:223-224)
-        *reinterpret_cast<uint32_t *>(ai + 16) = 0u;       // n_spent never incremented (Q14)
-        *reinterpret_cast<uint32_t *>(ai + 20) = 0u;
-        *reinterpret_cast<uint32_t *>(ai + 24) = 0u;
-        *reinterpret_cast<uint32_t *>(ai + 28) = Q.n_added_cards;
-        e.rew[q] = rw;
-      }
-    }
+    if (COG_HEX_END(c) || pv->turn_counter >= pv->max_steps) finish_episode(e);
   }
 }
 
@@ -1051,12 +1055,13 @@ __global__ void __launch_bounds__(256) k_encode_lds(const uint8_t *__restrict__ 
 }
 
 // ---- per-work-item LDS staging of a step's working set -------------------------------------
-// slot = 121 dwords (odd stride: same-offset dword accesses of a wave are bank-conflict free)
+// slot = 145 dwords (odd stride: same-offset dword accesses of a wave are bank-conflict free)
 //   [  0,128) EnvPriv line            [128,224) selected ActionMask (96 B)
 //   [224,272) ObsData 16128..16175 (phase, resources, shop)
-//   [272,384) DeckObs of the acting player (112 B)   [384,480) its stored ActionMask (96 B)
-constexpr int kSlotWords = 121;
-constexpr int SLOT_PV = 0, SLOT_SEL = 128, SLOT_SH = 224, SLOT_DK = 272, SLOT_ST = 384;
+//   [272,384) DeckObs of the acting player a0 (112 B)   [384,480) stored ActionMask of a0
+//   [480,576) stored ActionMask of the next player na (prefetched for the turn change)
+constexpr int kSlotWords = 145;
+constexpr int SLOT_PV = 0, SLOT_SEL = 128, SLOT_SH = 224, SLOT_DK = 272, SLOT_ST = 384, SLOT_STN = 480;
 
 DEV void stage_in(uint32_t *slot, int off, const uint8_t *g, int n16) {
   const uint4 *src = reinterpret_cast<const uint4 *>(g);
@@ -1069,12 +1074,304 @@ DEV void stage_in(uint32_t *slot, int off, const uint8_t *g, int n16) {
     }
   }
 }
-DEV void stage_out(const uint32_t *slot, int off, uint8_t *g, int n16) {
+// store the 16-B granules of a staged record whose bit is set in `dirty`
+DEV void stage_out(const uint32_t *slot, int off, uint8_t *g, int n16, uint32_t dirty = 0xffu) {
   uint4 *dst = reinterpret_cast<uint4 *>(g);
   const uint32_t *src = slot + off / 4;
 #pragma unroll
   for (int q = 0; q < 8; q++)
-    if (q < n16) dst[q] = make_uint4(src[4 * q], src[4 * q + 1], src[4 * q + 2], src[4 * q + 3]);
+    if (q < n16 && ((dirty >> q) & 1u)) dst[q] = make_uint4(src[4 * q], src[4 * q + 1], src[4 * q + 2], src[4 * q + 3]);
+}
+
+// ---- fast path: play / pass / turn change on registers (environment.cpp:91-250) -------------
+// Selected and stored masks are held as five head bitsets (bit k == index k of the head); the
+// deck's bulk operations run on dwords with compile-time byte positions.  Move / shop / remove /
+// special actions and resets take the byte-level path above (env_step / env_reset).
+struct Heads {
+  uint32_t play, spec, rem, move, shop;
+};
+
+DEV Heads heads_from(const uint8_t *mask) {               // ActionMask bytes -> bitsets
+  const uint32_t *m32 = reinterpret_cast<const uint32_t *>(mask);
+  uint64_t lo = 0, hi = 0;
+#pragma unroll
+  for (int w = 0; w < 23; w++) {
+    const uint64_t b = bools4(m32[w]);
+    if (4 * w < 64) lo |= b << (4 * w);
+    else hi |= b << (4 * w - 64);
+  }
+  Heads h;
+  h.play = (uint32_t)(lo & 0x3fffffu);
+  h.spec = (uint32_t)((lo >> 22) & 0x3fffffu);
+  h.rem = (uint32_t)(((lo >> 44) | (hi << 20)) & 0x3fffffu);
+  h.move = (uint32_t)((hi >> 2) & 0x7fu);
+  h.shop = (uint32_t)((hi >> 9) & 0x7ffffu);
+  return h;
+}
+DEV uint32_t expand4(uint32_t x) { return (x * 0x00204081u) & 0x01010101u; }   // 4 bits -> 4 bool bytes
+DEV void heads_to(const Heads &h, uint32_t *m32) {        // bitsets -> the 23 named dwords
+  const uint64_t lo = (uint64_t)h.play | ((uint64_t)h.spec << 22) | ((uint64_t)h.rem << 44);
+  const uint64_t hi = ((uint64_t)h.rem >> 20) | ((uint64_t)h.move << 2) | ((uint64_t)h.shop << 9);
+#pragma unroll
+  for (int w = 0; w < 23; w++)
+    m32[w] = expand4((uint32_t)((4 * w < 64 ? lo >> (4 * w) : hi >> (4 * w - 64)) & 0xfu));
+}
+DEV void sample_heads(const Heads &h, uint32_t &rng, uint8_t out[5]) {      // sampler.h:14-79
+  out[0] = pick(rng, h.play);
+  out[1] = pick(rng, h.spec);
+  out[2] = pick(rng, h.rem);
+  out[3] = pick(rng, h.move);
+  out[4] = pick(rng, h.shop);
+}
+DEV uint32_t set_bit(uint32_t m, int k, bool v) { return v ? (m | (1u << k)) : (m & ~(1u << k)); }
+
+constexpr cog_card_t kCards[COG_N_CARDTYPES] = COG_CARD_TABLE;
+constexpr uint8_t kShopTypes[COG_N_SHOP] = COG_SHOP_TYPES;
+constexpr uint32_t kSpecialBits = 0x1f8000u;              // card types 15..20
+
+DEV uint32_t byte_of(const uint32_t *w, int idx) { return (w[idx >> 2] >> (8 * (idx & 3))) & 0xffu; }
+DEV void put_byte(uint32_t *w, int idx, uint32_t v) {
+  const int sh = 8 * (idx & 3);
+  w[idx >> 2] = (w[idx >> 2] & ~(0xffu << sh)) | ((v & 0xffu) << sh);
+}
+
+// Deck::discard_all_active + discard_all_played (cards.cpp:219-232) on dwords 10..26
+DEV void fast_discard_all(uint32_t *dk32) {
+  uint32_t w[17];
+#pragma unroll
+  for (int q = 0; q < 17; q++) w[q] = dk32[10 + q];
+#pragma unroll
+  for (int k = 0; k < COG_N_CARDTYPES; k++) {
+    const uint32_t a = byte_of(w, COG_DECK_ACTIVE + k - 40), p = byte_of(w, COG_DECK_PLAYED + k - 40);
+    put_byte(w, COG_DECK_DISCARD + k - 40, byte_of(w, COG_DECK_DISCARD + k - 40) + a + p);
+    put_byte(w, COG_DECK_ACTIVE + k - 40, 0u);
+    put_byte(w, COG_DECK_PLAYED + k - 40, 0u);
+  }
+#pragma unroll
+  for (int q = 0; q < 17; q++) dk32[10 + q] = w[q];
+}
+
+// Deck::move_discard_to_draw (cards.cpp:234-240): draw dwords 0..5, discard dwords 21..26
+DEV void fast_move_discard_to_draw(uint32_t *dk32, PlayerPriv &P) {
+  uint32_t d[6], x[6];
+#pragma unroll
+  for (int q = 0; q < 6; q++) { d[q] = dk32[q]; x[q] = dk32[21 + q]; }
+  uint32_t nd = P.n_in_draw;
+#pragma unroll
+  for (int k = 0; k < COG_N_CARDTYPES; k++) {
+    const uint32_t v = byte_of(x, k);                      // discard byte 84+k == x byte k
+    put_byte(d, k, byte_of(d, k) + v);
+    nd += v;
+    put_byte(x, k, 0u);
+  }
+  P.n_in_draw = (uint8_t)nd;
+#pragma unroll
+  for (int q = 0; q < 6; q++) { dk32[q] = d[q]; dk32[21 + q] = x[q]; }
+}
+
+// hand[k] > 0 for k < 21 as a bitset (hand = bytes 21..41 = dwords 5..10)
+DEV uint32_t hand_bits(const uint32_t *dk32) {
+  uint32_t w[6];
+#pragma unroll
+  for (int q = 0; q < 6; q++) w[q] = dk32[5 + q];
+  uint32_t h = 0;
+#pragma unroll
+  for (int k = 0; k < COG_N_CARDTYPES; k++) h |= (byte_of(w, COG_DECK_HAND + k - 20) != 0u ? 1u : 0u) << k;
+  return h;
+}
+DEV void fast_enable_playing(const uint32_t *dk32, Heads &sel) {   // player.cpp:198-206
+  const uint32_t h = hand_bits(dk32);
+  sel.rem = 1u;
+  sel.play = 1u | (h << 1);
+  sel.spec = 1u | ((h & kSpecialBits) << 1);
+}
+
+// Deck::draw (cards.cpp:183-211); the draw-pile scan runs on registers.  n_in_draw equals the
+// sum of draw[] mod 256 (every Deck operation keeps it), so t < n_in_draw always ends inside
+// draw[0..20]; the guard only raises the hazard flag.
+DEV void fast_draw(const Ctx &e, PlayerPriv &P, uint32_t *dk32, Heads &sel, uint32_t &rng, uint8_t n) {
+  if (P.n_in_draw < n) fast_move_discard_to_draw(dk32, P);
+  if (n > P.n_in_draw) n = P.n_in_draw;
+  if (!n) return;
+  uint32_t d[6];
+#pragma unroll
+  for (int q = 0; q < 6; q++) d[q] = dk32[q];
+  for (int i = 0; i < n; i++) {
+    uint32_t t = uid(rng, P.n_in_draw);
+    int c = COG_N_CARDTYPES;
+#pragma unroll
+    for (int k = 0; k < COG_N_CARDTYPES; k++) {
+      const uint32_t v = byte_of(d, k);
+      if (c == COG_N_CARDTYPES) {
+        if (t >= v) t -= v;
+        else c = k;
+      }
+    }
+    if (c == COG_N_CARDTYPES) {                            // unreachable (see above)
+      e.pv->flags |= F_SCAN_OVER;
+      c = COG_N_CARDTYPES - 1;
+    }
+#pragma unroll
+    for (int q = 0; q < 6; q++)
+      if (q == (c >> 2)) d[q] -= 1u << (8 * (c & 3));      // draw[c] >= 1: no borrow
+    P.n_in_draw--;
+    e.dka[COG_DECK_HAND + c]++;
+    sel.play |= 1u << (c + 1);
+    sel.spec = set_bit(sel.spec, c + 1, is_special(c));
+  }
+#pragma unroll
+  for (int q = 0; q < 5; q++) dk32[q] = d[q];
+  e.dka[20] = (uint8_t)byte_of(d, 20);                     // bytes 21..23 are hand[0..2]
+  P.n_in_hand = (uint8_t)(P.n_in_hand + n);
+}
+
+// bytes 66..91 (move[0..6], get_from_shop[0..18]) of a stored mask from two bitsets
+DEV void put_move_shop(uint32_t *st32, uint32_t move, uint32_t shop) {
+  const uint32_t v = move | (shop << 7);
+  st32[16] = (st32[16] & 0xffffu) | ((v & 1u) << 16) | (((v >> 1) & 1u) << 24);
+#pragma unroll
+  for (int q = 0; q < 6; q++) st32[17 + q] = expand4((v >> (2 + 4 * q)) & 0xfu);
+}
+
+struct Cells {                        // own cell [0] and neighbours [1..6] of one player
+  uint8_t c[7];
+  uint8_t oob;                        // bit d: lookup d fell outside the map (flag only if used)
+};
+DEV Cells prefetch_cells(const Ctx &e, int player) {      // Map::get_from_array, no side effects
+  const EnvPriv *pv = e.pv;
+  Cells r;
+  r.oob = 0;
+  const int lx = pv->locx[player], ly = pv->locy[player];
+#pragma unroll
+  for (int d = 0; d < 7; d++) {
+    const int ix = lx + c_dirs[d][0] / 2 - pv->minx + 1, iy = ly + c_dirs[d][1] / 2 - pv->miny + 1;
+    const bool out = ix < 0 || iy < 0 || ix >= pv->dimx || iy >= pv->dimy;
+    const bool ring = ix >= COG_GRID || iy >= COG_GRID;
+    const int cx = min(max(ix, 0), COG_GRID - 1), cy = min(max(iy, 0), COG_GRID - 1);
+    const uint8_t v = e.cgrid[cx * COG_GRID + cy];
+    r.c[d] = (out || ring || !v) ? (uint8_t)COG_HEX_MOUNTAIN : v;
+    r.oob |= (uint8_t)((out ? 1u : 0u) << d);
+  }
+  return r;
+}
+DEV uint8_t use_cell(const Ctx &e, const Cells &c, int d) {
+  if ((c.oob >> d) & 1u) e.pv->flags |= F_OOB_LOOKUP;
+  return c.c[d];
+}
+
+// movement mask bits 1..6 (map.cpp:369-387) + bit 0
+DEV uint32_t move_bits(const Ctx &e, const Cells &cl, float r0, float r1, float r2, uint8_t n_active) {
+  uint32_t m = 1u;
+#pragma unroll
+  for (int d = 1; d < 7; d++) {
+    const uint8_t c = use_cell(e, cl, d);
+    const int req = COG_HEX_REQ(c);
+    const uint32_t n = COG_HEX_N(c);
+    const float r = req == 0 ? r0 : (req == 1 ? r1 : r2);
+    const bool filled = req >= COG_REQ_DISCARD ? n_active > n : r >= (float)n;
+    if (req != COG_REQ_NULL && filled) m |= 1u << d;
+  }
+  return m;
+}
+// shop mask bits 1..18 (cards.cpp:109-121) + bit 0
+DEV uint32_t shop_bits(const Ctx &e, float coins) {
+  const bool few = e.pv->n_in_market < COG_MKT_SLOTS;
+  const uint32_t im = e.pv->in_market;
+  uint32_t m = 1u;
+#pragma unroll
+  for (int i = 0; i < COG_N_SHOP; i++) {
+    const bool ok = few ? e.sh[SH_SHOP + i] > 0 : ((im >> i) & 1u);
+    if (ok && coins > (float)kCards[kShopTypes[i]].cost) m |= 1u << (i + 1);
+  }
+  return m;
+}
+
+struct FastOut {
+  bool turn_end;
+  uint32_t dirty_dk, dirty_st;        // 16-B granules of the staged deck / stored mask of a0
+};
+
+// cog_env::step for play / pass actions (environment.cpp:91-107, 128-150 pass branch, 176-207)
+DEV FastOut fast_step(const Ctx &e, const uint8_t act[5], Heads &sel, uint8_t *stn, const Cells cl[2], int na) {
+  FastOut o{false, 0u, 0u};
+  EnvPriv *pv = e.pv;
+  const int ag = pv->agent;
+  uint8_t phase = e.sh[0];
+  if (phase == COG_PHASE_INACTIVE) phase = COG_PHASE_MOVEMENT;
+  PlayerPriv &P = pv->pl[ag];
+  P.steps_taken++;
+  float *res3 = res(e);
+  float r0 = res3[0], r1 = res3[1], r2 = res3[2];
+  uint32_t *dk32 = reinterpret_cast<uint32_t *>(e.dka);
+  if (act[0]) {                                            // Player::play_card + Deck::activate
+    const int c = (uint8_t)(act[0] - 1);
+    if (phase == COG_PHASE_MOVEMENT) {
+      r0 = (float)c_cards[c].res[0]; r1 = (float)c_cards[c].res[1]; r2 = (float)c_cards[c].res[2];
+    } else if (phase == COG_PHASE_BUYING) {
+      const uint8_t coin = c_cards[c].res[2];
+      r2 = r2 + (coin > 0 ? (float)coin : 0.5f);
+    }
+    P.n_in_hand--;
+    P.n_active++;
+    P.idx_last = (uint8_t)c;
+    const uint8_t prev = e.dka[COG_DECK_HAND + c];
+    e.dka[COG_DECK_HAND + c] = (uint8_t)(prev - 1);
+    e.dka[COG_DECK_ACTIVE + c]++;
+    const bool pl = prev > 1;
+    sel.play = set_bit(sel.play, c + 1, pl);
+    sel.spec = set_bit(sel.spec, c + 1, pl && is_special(c));
+    o.dirty_dk |= (1u << ((COG_DECK_HAND + c) >> 4)) | (1u << ((COG_DECK_ACTIVE + c) >> 4));
+  } else {                                                 // pass
+    P.next_move_free = 0;
+    phase = (uint8_t)((phase + 1) % 3);
+    if (P.n_removes > 0) {
+      P.n_removes = 0;
+      fast_enable_playing(dk32, sel);
+    }
+    if (P.next_card_free) {
+      P.next_card_free = 0;
+      fast_enable_playing(dk32, sel);
+    }
+  }
+  if (P.mip && !act[3]) {                                  // the move HEAD, even when play won
+    P.mip = 0;
+    r0 = r1 = r2 = 0.f;
+  }
+  int cur = ag;
+  if (P.has_won || phase == COG_PHASE_INACTIVE) {          // maybe_end_turn -> next_agent
+    o.turn_end = true;
+    P.n_active = 0;                                        // Player::end_turn (player.cpp:170-180)
+    fast_discard_all(dk32);
+    const int n_draw = COG_HAND_SIZE - (int)P.n_in_hand;
+    if (n_draw > 0) {
+      uint32_t rng = pv->rng;
+      fast_draw(e, P, dk32, sel, rng, (uint8_t)n_draw);
+      pv->rng = rng;
+    }
+    heads_to(sel, reinterpret_cast<uint32_t *>(e.sta));  // save_actionmask
+    o.dirty_dk = 0x7fu;
+    o.dirty_st = 0x3fu;
+    pv->agent = (uint8_t)na;
+    sel = heads_from(na == ag ? e.sta : stn);             // load_actionmask
+    r0 = r1 = r2 = 0.f;
+    pv->turn_counter++;
+    cur = na;
+  }
+  e.sh[0] = phase;
+  res3[0] = r0; res3[1] = r1; res3[2] = r2;
+  const Cells &cc = cur == ag ? cl[0] : cl[1];
+  uint32_t mv = 1u, sp = 1u;                               // update_observation (:252-279)
+  if (phase == COG_PHASE_MOVEMENT) mv = move_bits(e, cc, r0, r1, r2, pv->pl[cur].n_active);
+  else if (phase == COG_PHASE_BUYING) sp = shop_bits(e, r2);
+  if (cur == ag) {
+    put_move_shop(reinterpret_cast<uint32_t *>(e.sta), mv, sp);
+    o.dirty_st |= 0x30u;
+  } else {
+    put_move_shop(reinterpret_cast<uint32_t *>(stn), mv, sp);
+  }
+  const uint8_t c = use_cell(e, cc, 0);                    // done check (:187)
+  if (COG_HEX_END(c) || pv->turn_counter >= pv->max_steps) finish_episode(e);
+  return o;
 }
 
 // One env step (optionally preceded by sampling its action), state staged through LDS.
@@ -1091,10 +1388,12 @@ DEV void staged_step(const DevState &s, uint32_t *slot, size_t i, const uint8_t 
   uint8_t *lds = reinterpret_cast<uint8_t *>(slot);
   EnvPriv *pv = reinterpret_cast<EnvPriv *>(lds + SLOT_PV);
   const int a0 = pv->agent;
+  const int na = a0 + 1 >= pv->n_players ? 0 : a0 + 1;
   uint8_t *gdk = ob + COG_OBS_PLAYER0 + COG_OBS_PLAYER_STRIDE * a0;
+  uint8_t *gstn = ob + COG_OBS_PLAYER0 + COG_OBS_PLAYER_STRIDE * na + COG_PD_MASK;
   stage_in(slot, SLOT_DK, gdk, 7);
   stage_in(slot, SLOT_ST, gdk + COG_PD_MASK, 6);
-  STAMP(s, 1);
+  stage_in(slot, SLOT_STN, gstn, 6);
 
   Ctx e;
   e.ob = ob;
@@ -1109,22 +1408,50 @@ DEV void staged_step(const DevState &s, uint32_t *slot, size_t i, const uint8_t 
   e.grid = s.grid + i * (size_t)kGridBytes;
   e.cgrid = s.cgrid + i * COG_CELLS;
   e.gs = s.gen + i;
+  Cells cl[2];
+  cl[0] = prefetch_cells(e, a0);
+  cl[1] = prefetch_cells(e, na);
+  uint8_t *ginfo_steps = e.info + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * a0;
+  const uint8_t info_steps = *ginfo_steps;
+  STAMP(s, 1);
 
+  Heads sel = heads_from(e.sel);
   uint8_t act[5];
   if (act_in) {
     for (int k = 0; k < 5; k++) act[k] = act_in[k];
   } else {                                                 // runner: sample(selected | stored mask)
     uint32_t rng = rngs[i];
-    sample_mask(mask_source == MASK_STORED ? e.sta : e.sel, rng, act);
+    if (mask_source == MASK_STORED) sample_heads(heads_from(e.sta), rng, act);
+    else sample_heads(sel, rng, act);
     rngs[i] = rng;
     store_action(actions_out + i * COG_ACTION_BYTES, act);
   }
   STAMP(s, 2);
-  env_step(e, act);
+  const bool fast = !pv->done && (act[0] != 0 || (act[1] == 0 && act[2] == 0 && act[3] == 0 && act[4] == 0));
+  FastOut fo{false, 0x7fu, 0x3fu};
+  uint32_t dirty_pv = 0xffu, dirty_sh = 0x7u;
+  bool sel_in_regs = false;
+  if (fast) {
+    *ginfo_steps = (uint8_t)(info_steps + 1);              // agent_infos[a].steps_taken += 1
+    fo = fast_step(e, act, sel, lds + SLOT_STN, cl, na);
+    sel_in_regs = true;
+    dirty_pv = 0x3u | (1u << (4 + a0));
+    dirty_sh = 0x1u;
+  } else {
+    env_step(e, act);
+  }
   STAMP(s, 3);
   const uint8_t done = pv->done;
   s.done[i] = done;                                        // dones[i] before the auto-reset
+  if (fast && fo.turn_end && na != a0)                      // next player's refreshed move / shop bytes
+    stage_out(slot, SLOT_STN, gstn, 6, 0x30u);
   if (done) {                                              // vec_environment.h:56-59
+    if (sel_in_regs) heads_to(sel, reinterpret_cast<uint32_t *>(e.sel));
+    sel_in_regs = false;
+    fo.dirty_dk = 0x7fu;
+    fo.dirty_st = 0x3fu;
+    dirty_pv = 0xffu;
+    dirty_sh = 0x7u;
     if (!env_reset(e)) {
       atomicOr(&s.status[0], pv->flags);
       atomicAdd(&s.status[1], 1u);
@@ -1136,11 +1463,20 @@ DEV void staged_step(const DevState &s, uint32_t *slot, size_t i, const uint8_t 
   }
   s.agent[i] = pv->agent;
   STAMP(s, 4);
-  stage_out(slot, SLOT_PV, gpv, 8);
-  stage_out(slot, SLOT_SEL, gsel, 6);
-  stage_out(slot, SLOT_SH, ob + COG_OBS_PHASE, 3);
-  stage_out(slot, SLOT_DK, gdk, 7);
-  stage_out(slot, SLOT_ST, gdk + COG_PD_MASK, 6);
+  if (sel_in_regs) {
+    uint32_t m[24];
+    heads_to(sel, m);
+    m[23] = 0u;
+    uint4 *d = reinterpret_cast<uint4 *>(gsel);
+#pragma unroll
+    for (int q = 0; q < 6; q++) d[q] = make_uint4(m[4 * q], m[4 * q + 1], m[4 * q + 2], m[4 * q + 3]);
+  } else {
+    stage_out(slot, SLOT_SEL, gsel, 6);
+  }
+  stage_out(slot, SLOT_PV, gpv, 8, dirty_pv);
+  stage_out(slot, SLOT_SH, ob + COG_OBS_PHASE, 3, dirty_sh);
+  stage_out(slot, SLOT_DK, gdk, 7, fo.dirty_dk);
+  stage_out(slot, SLOT_ST, gdk + COG_PD_MASK, 6, fo.dirty_st);
   STAMP(s, 5);
 }
 
