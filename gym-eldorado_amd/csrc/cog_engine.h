@@ -8,9 +8,9 @@
 //   sel   [N] x 128 B     selected ActionMask (the deck's mask, player.cpp:16-27)
 //   info  [N] x 192 B     Info records
 //   rew   [N] x 4 f32, done [N] u8, agent [N] u8
-//   priv  [N] x 128 B     EnvPriv: everything the reference keeps in private members
+//   priv  [N] x 160 B     EnvPriv: everything the reference keeps in private members
 //                         (rng, turn counter, Player/Deck/Shop counters, player locations,
-//                         map bounds) -- one 128-B line per env
+//                         map bounds) + a cache of each player's 7 neighbourhood hex codes
 //   grid  [N] x 16384 B   absolute-coordinate hex-code grid, 128 x 128 cells, cell (x, y) at
 //                         (x + 64) * 128 + (y + 64); 0 = no hex.  Built by map generation,
 //                         read by movement masks, done checks and the map-observation encode.
@@ -42,6 +42,7 @@ constexpr uint32_t F_GRID_OVER = 0x10u;
 constexpr uint32_t F_OOB_LOOKUP = 0x20u;
 constexpr uint32_t F_SCAN_OVER = 0x40u;
 constexpr uint32_t F_B_START_LT4 = 0x80u;
+constexpr uint32_t F_BAD_ACTION = 0x100u;
 constexpr uint32_t F_ERROR_MASK = F_MAPGEN_FAIL | F_GRID_OVER;
 
 struct PlayerPriv {                  // Player + Deck private members (player.h:60-75, cards.h:137-145)
@@ -64,10 +65,13 @@ struct EnvPriv {                    // cog_env private members (environment.h:12
   int8_t minx, miny, maxx, maxy;     // Map::min_xy / max_xy (integer hex coords)
   uint8_t dimx, dimy, pad0, pad1b;
   int8_t locx[4], locy[4];           // Map::player_locations
-  uint32_t pad1[4];
+  uint8_t info_steps[4];             // mirror of Info.agent_infos[p].steps_taken (never read back)
+  uint32_t pad1[3];
   PlayerPriv pl[4];
+  uint8_t cells[4][8];               // per player: hex codes of its cell [0] and neighbours [1..6]
+                                     // as Map::get_from_array returns them, [7] = out-of-map bits
 };
-static_assert(sizeof(EnvPriv) == 128, "EnvPriv is one 128-B line");
+static_assert(sizeof(EnvPriv) == 160, "EnvPriv is ten 16-B granules");
 
 struct alignas(64) GenScratch {
   uint8_t pieces[kMaxPlaced];

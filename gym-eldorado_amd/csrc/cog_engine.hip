@@ -38,11 +38,12 @@ DEV unsigned long long stamp_clock() {
   do {                                                                                       \
     const unsigned long long t_ = stamp_clock();                                             \
     if ((s).stamps && (threadIdx.x & 63) == 0)                                               \
-      (s).stamps[((size_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 8 + (k)] = t_; \
+      (s).stamps[((size_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 16 + (k)] = t_; \
   } while (0)
 #else
 #define STAMP(s, k) do { } while (0)
 #endif
+#define STAMP_AT(k) STAMP(e, k)     // inside step functions: Ctx carries the stamp buffer
 
 namespace cog {
 
@@ -94,6 +95,7 @@ DEV uint32_t uid(uint32_t &x, uint32_t k) {
 // per-env context
 // ------------------------------------------------------------------------------------------
 struct Ctx {
+  unsigned long long *stamps;   // diagnostic builds only (STAMP_AT)
   uint8_t *ob;        // ObsData record (global): map, decks / stored masks of other players
   uint8_t *sh;        // shared block = ObsData bytes 16128..16175 (phase @0, resources @4, shop @16)
   uint8_t *dka;       // DeckObs of player a0 (staged copy in LDS, or global)
@@ -123,6 +125,7 @@ DEV Ctx make_ctx(const DevState &s, size_t i) {
   e.grid = s.grid + i * (size_t)kGridBytes;
   e.cgrid = s.cgrid + i * COG_CELLS;
   e.gs = s.gen + i;
+  e.stamps = nullptr;
   return e;
 }
 
@@ -152,6 +155,27 @@ DEV uint8_t lookup(const Ctx &e, int x, int y) {
   if (ix >= COG_GRID || iy >= COG_GRID) return COG_HEX_MOUNTAIN;   // ring cell of a 49-wide map
   const uint8_t c = e.cgrid[ix * COG_GRID + iy];
   return c ? c : (uint8_t)COG_HEX_MOUNTAIN;
+}
+
+// the neighbourhood cache of one player (EnvPriv::cells): the codes lookup() returns for its
+// cell and its six neighbours, and which of those seven lookups fall outside the map (the
+// OOB_LOOKUP flag is raised when a cached cell is USED, as the reference's lookups would be)
+DEV void load_cells(const Ctx &e, int player) {
+  const EnvPriv *pv = e.pv;
+  uint8_t *out = e.pv->cells[player];
+  const int lx = pv->locx[player], ly = pv->locy[player];
+  uint32_t oob = 0;
+#pragma unroll
+  for (int d = 0; d < 7; d++) {
+    const int ix = lx + c_dirs[d][0] / 2 - pv->minx + 1, iy = ly + c_dirs[d][1] / 2 - pv->miny + 1;
+    const bool out_ = ix < 0 || iy < 0 || ix >= pv->dimx || iy >= pv->dimy;
+    const bool ring = ix >= COG_GRID || iy >= COG_GRID;
+    const int cx = min(max(ix, 0), COG_GRID - 1), cy = min(max(iy, 0), COG_GRID - 1);
+    const uint8_t v = e.cgrid[cx * COG_GRID + cy];
+    out[d] = (out_ || ring || !v) ? (uint8_t)COG_HEX_MOUNTAIN : v;
+    oob |= (out_ ? 1u : 0u) << d;
+  }
+  out[7] = (uint8_t)oob;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -202,131 +226,11 @@ DEV void deck_draw(const Ctx &e, int p, uint8_t n) {        // cards.cpp:183-211
   P.n_in_hand = (uint8_t)(P.n_in_hand + n);
 }
 
-DEV void deck_activate(const Ctx &e, int p, int c) {        // cards.cpp:242-253
-  PlayerPriv &P = e.pv->pl[p];
-  uint8_t *d = deck(e, p);
-  P.n_in_hand--;
-  P.n_active++;
-  P.idx_last = (uint8_t)c;
-  const uint8_t prev = d[COG_DECK_HAND + c];
-  d[COG_DECK_HAND + c] = (uint8_t)(prev - 1);
-  d[COG_DECK_ACTIVE + c]++;
-  const uint8_t pl = prev > 1;
-  e.sel[COG_MASK_PLAY + 1 + c] = pl;
-  e.sel[COG_MASK_SPECIAL + 1 + c] = pl && is_special(c);
-}
-
-DEV void deck_play_last_activated(const Ctx &e, int p) {    // cards.cpp:255-261
-  PlayerPriv &P = e.pv->pl[p];
-  uint8_t *d = deck(e, p);
-  P.n_active--;
-  d[COG_DECK_ACTIVE + P.idx_last]--;
-  if (!c_cards[P.idx_last].single_use) d[COG_DECK_PLAYED + P.idx_last]++;
-}
-
-DEV void deck_play_immediate(const Ctx &e, int p, int c) {  // cards.cpp:263-273
-  PlayerPriv &P = e.pv->pl[p];
-  uint8_t *d = deck(e, p);
-  P.n_in_hand--;
-  const uint8_t prev = d[COG_DECK_HAND + c];
-  d[COG_DECK_HAND + c] = (uint8_t)(prev - 1);
-  d[COG_DECK_PLAYED + c]++;
-  const uint8_t pl = prev > 1;
-  e.sel[COG_MASK_PLAY + 1 + c] = pl;
-  e.sel[COG_MASK_SPECIAL + 1 + c] = pl && is_special(c);
-}
-
-DEV void deck_remove_immediate(const Ctx &e, int p, int c) { // cards.cpp:281-290
-  PlayerPriv &P = e.pv->pl[p];
-  uint8_t *d = deck(e, p);
-  P.n_in_hand--;
-  const uint8_t prev = d[COG_DECK_HAND + c];
-  d[COG_DECK_HAND + c] = (uint8_t)(prev - 1);
-  e.sel[COG_MASK_REMOVE + 1 + c] = e.sel[COG_MASK_REMOVE + 1 + c] && prev > 1;
-  const uint8_t pl = e.sel[COG_MASK_PLAY + 1 + c] && prev > 1;
-  e.sel[COG_MASK_PLAY + 1 + c] = pl;
-  e.sel[COG_MASK_SPECIAL + 1 + c] = pl && is_special(c);
-}
-
-DEV void disable_playing(const Ctx &e) {                    // player.cpp:191-196
-  for (int k = 0; k < 22; k++) {
-    e.sel[COG_MASK_PLAY + k] = k == 0;
-    e.sel[COG_MASK_SPECIAL + k] = k == 0;
-  }
-}
-
-DEV void enable_playing(const Ctx &e, int p) {              // player.cpp:198-206
-  const uint8_t *d = deck(e, p);
-  e.sel[COG_MASK_REMOVE] = 1;
-  for (int k = 1; k < 22; k++) {
-    e.sel[COG_MASK_REMOVE + k] = 0;
-    const uint8_t pl = d[COG_DECK_HAND + k - 1] > 0;
-    e.sel[COG_MASK_PLAY + k] = pl;
-    e.sel[COG_MASK_SPECIAL + k] = pl && is_special(k - 1);
-  }
-}
-
-DEV void cards_from_active(const Ctx &e, int p, uint8_t n, bool discard) {  // player.cpp:85-131
-  PlayerPriv &P = e.pv->pl[p];
-  uint8_t *d = deck(e, p);
-  const uint8_t avail = P.n_active;
-  if (n > avail) {
-    if (discard) e.pv->flags |= F_Q24_CLAMP;
-    n = avail;
-  }
-  uint32_t rng = e.pv->rng;
-  for (uint8_t i = 0; i < n; i++) {
-    const uint32_t t = uid(rng, (uint32_t)(avail - i));
-    const int c = scan(e, d, COG_DECK_ACTIVE, t);
-    P.n_active--;
-    d[COG_DECK_ACTIVE + c]--;
-    if (discard) d[COG_DECK_DISCARD + c]++;
-  }
-  e.pv->rng = rng;
-}
-
-DEV void handle_requirement(const Ctx &e, int p, int req, uint8_t n) {  // player.cpp:141-162
-  PlayerPriv &P = e.pv->pl[p];
-  float *r = res(e);
-  if (req < 3) {
-    const float left = r[req] - (float)n;
-    r[0] = 0.f; r[1] = 0.f; r[2] = 0.f;
-    r[req] = left;
-    if (!P.mip) {
-      deck_play_last_activated(e, p);
-      P.mip = 1;
-    }
-  } else if (req == COG_REQ_REMOVE || req == COG_REQ_DISCARD) {
-    cards_from_active(e, p, n, req == COG_REQ_DISCARD);
-    r[0] = 0.f; r[1] = 0.f; r[2] = 0.f;
-    P.mip = 0;
-  }
-}
-
 DEV void copy_mask(uint8_t *dst, const uint8_t *src) {     // ActionMask copy (named fields)
   const uint32_t *s = reinterpret_cast<const uint32_t *>(src);   // 4-byte aligned (LDS slots)
   uint32_t *d = reinterpret_cast<uint32_t *>(dst);
 #pragma unroll
   for (int k = 0; k < 23; k++) d[k] = s[k];                // bytes 0..91: the named fields
-}
-
-DEV void end_turn(const Ctx &e, int p) {                   // player.cpp:170-180
-  PlayerPriv &P = e.pv->pl[p];
-  uint8_t *d = deck(e, p);
-  P.n_active = 0;
-  for (int i = 0; i < COG_N_CARDTYPES; i++) {
-    d[COG_DECK_DISCARD + i] = (uint8_t)(d[COG_DECK_DISCARD + i] + d[COG_DECK_ACTIVE + i]);
-    d[COG_DECK_ACTIVE + i] = 0;
-  }
-  for (int i = 0; i < COG_N_CARDTYPES; i++) {
-    d[COG_DECK_DISCARD + i] = (uint8_t)(d[COG_DECK_DISCARD + i] + d[COG_DECK_PLAYED + i]);
-    d[COG_DECK_PLAYED + i] = 0;
-  }
-  const int n_draw = COG_HAND_SIZE - (int)P.n_in_hand;
-  if (n_draw > 0) deck_draw(e, p, (uint8_t)n_draw);
-  float *r = res(e);
-  r[0] = 0.f; r[1] = 0.f; r[2] = 0.f;
-  copy_mask(stm(e, p), e.sel);
 }
 
 DEV void shop_mask(const Ctx &e, float coins, uint8_t *mask) {  // cards.cpp:109-121
@@ -338,17 +242,6 @@ DEV void shop_mask(const Ctx &e, float coins, uint8_t *mask) {  // cards.cpp:109
     const bool ok = few ? avail[i] > 0 : ((im >> i) & 1u);
     mask[i + 1] = ok && (coins > cost);
   }
-}
-
-DEV int shop_get(const Ctx &e, int k) {                    // cards.cpp:136-142
-  uint8_t *avail = e.sh + SH_SHOP;
-  const uint8_t a = (uint8_t)(avail[k] - 1);
-  avail[k] = a;
-  if (!a && ((e.pv->in_market >> k) & 1u)) {
-    e.pv->in_market &= ~(1u << k);
-    e.pv->n_in_market--;
-  }
-  return c_shop_types[k];
 }
 
 DEV void movement_mask(const Ctx &e, uint8_t *move, int player, const float *r, uint8_t n_active) {
@@ -402,42 +295,6 @@ DEV void player_reset(const Ctx &e, int p) {               // player.cpp:29-43
   P.n_in_draw = 0; P.n_in_hand = 0; P.n_active = 0;
   deck_draw(e, p, COG_HAND_SIZE);
   copy_mask(stm(e, p), e.sel);
-}
-
-// special actions (cards.cpp:8-36) and the remove-lambda (environment.cpp:156-158), applied to
-// the stored mask of the CURRENT agent and the ACTING player (environment.cpp:183-186)
-DEV void apply_special(const Ctx &e, int special, int p) {
-  uint8_t *mask = stm(e, e.pv->agent);
-  PlayerPriv &P = e.pv->pl[p];
-  switch (special) {
-    case COG_SPECIAL_DRAW2: deck_draw(e, p, 2); break;
-    case COG_SPECIAL_DRAW3: deck_draw(e, p, 3); break;
-    case COG_SPECIAL_DRAW1_REMOVE1:
-    case COG_SPECIAL_DRAW2_REMOVE2: {
-      const uint8_t k = special == COG_SPECIAL_DRAW1_REMOVE1 ? 1 : 2;
-      deck_draw(e, p, k);
-      P.n_removes = k;
-      for (int j = 0; j < 22; j++) mask[COG_MASK_REMOVE + j] = mask[COG_MASK_PLAY + j];
-      disable_playing(e);
-      shop_mask(e, 0.f, mask + COG_MASK_SHOP);
-    } break;
-    case COG_SPECIAL_TRANSMIT:
-      mask[COG_MASK_MOVE] = 1;
-      for (int k = 1; k < 7; k++) mask[COG_MASK_MOVE + k] = 0;
-      disable_playing(e);
-      for (int i = 0; i < COG_N_SHOP; i++) mask[COG_MASK_SHOP + 1 + i] = e.sh[SH_SHOP + i] > 0;
-      P.next_card_free = 1;
-      break;
-    case COG_SPECIAL_NATIVE: {
-      const float r100[3] = {100.f, 100.f, 100.f};
-      movement_mask(e, mask + COG_MASK_MOVE, p, r100, 100);
-      P.next_move_free = 1;
-      disable_playing(e);
-      shop_mask(e, 0.f, mask + COG_MASK_SHOP);
-    } break;
-    case COG_SPECIAL_SHOP_OFF: shop_mask(e, 0.f, mask + COG_MASK_SHOP); break;
-    default: break;
-  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -723,6 +580,7 @@ DEV bool env_reset(const Ctx &e) {
   pv->turn_counter = 0;
   for (int i = 0; i < pv->n_players; i++) update_observation(e, i);
   copy_mask(e.sel, stm(e, 0));
+  for (int i = 0; i < pv->n_players; i++) load_cells(e, i);
   return true;
 }
 
@@ -738,6 +596,7 @@ DEV void finish_episode(const Ctx &e) {
     uint8_t *ai = e.info + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * q;
     const float rw = (float)(pv->n_players * Q.has_won) - n_winners;
     ai[0] = Q.steps_taken;
+    pv->info_steps[q] = Q.steps_taken;
     *reinterpret_cast<float *>(ai + 4) = rw;
     *reinterpret_cast<uint32_t *>(ai + 8) = Q.n_movements;
     ai[12] = Q.n_added_cards;
@@ -747,93 +606,6 @@ DEV void finish_episode(const Ctx &e) {
     *reinterpret_cast<uint32_t *>(ai + 24) = 0u;
     *reinterpret_cast<uint32_t *>(ai + 28) = Q.n_added_cards;
     e.rew[q] = rw;
-  }
-}
-
-// cog_env::step (environment.cpp:91-224)
-DEV void env_step(const Ctx &e, const uint8_t *act) {
-  EnvPriv *pv = e.pv;
-  if (pv->done) return;
-  const uint8_t a_play = act[0], a_special = act[1], a_remove = act[2], a_move = act[3], a_shop = act[4];
-  const int ag = pv->agent;
-  e.info[COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag]++;  // agent_infos[a].steps_taken (u8)
-  if (e.sh[0] == COG_PHASE_INACTIVE) e.sh[0] = COG_PHASE_MOVEMENT;
-  PlayerPriv &P = pv->pl[ag];
-  P.steps_taken++;
-  float *r = res(e);
-  int special = COG_SPECIAL_NONE;
-  if (a_play) {
-    const int c = (uint8_t)(a_play - 1);
-    const uint8_t ph = e.sh[0];
-    if (ph == COG_PHASE_MOVEMENT) {
-      r[0] = (float)c_cards[c].res[0]; r[1] = (float)c_cards[c].res[1]; r[2] = (float)c_cards[c].res[2];
-    } else if (ph == COG_PHASE_BUYING) {
-      const uint8_t coin = c_cards[c].res[2];
-      r[2] = r[2] + (coin > 0 ? (float)coin : 0.5f);
-    }
-    deck_activate(e, ag, c);
-  } else if (a_special) {
-    const int c = (uint8_t)(a_special - 1);
-    if (c_cards[c].single_use) deck_remove_immediate(e, ag, c);
-    else deck_play_immediate(e, ag, c);
-    special = c_cards[c].special;
-  } else if (a_move) {
-    const int nx = pv->locx[ag] + c_dirs[a_move][0] / 2, ny = pv->locy[ag] + c_dirs[a_move][1] / 2;
-    pv->locx[ag] = (int8_t)nx;
-    pv->locy[ag] = (int8_t)ny;
-    const uint8_t c = lookup(e, nx, ny);
-    if (!P.next_move_free) handle_requirement(e, ag, COG_HEX_REQ(c), COG_HEX_N(c));
-    else { P.next_move_free = 0; enable_playing(e, ag); }
-    P.n_movements++;
-    P.has_won = COG_HEX_END(c);
-  } else {
-    P.next_move_free = 0;
-    if (a_shop) {
-      const int k = (uint8_t)(a_shop - 1);
-      int type;
-      if (P.next_card_free) {
-        type = shop_get(e, k);
-      } else {
-        const uint32_t was = (pv->in_market >> k) & 1u;
-        pv->n_in_market = (uint8_t)(pv->n_in_market + (uint8_t)(1u - was));
-        pv->in_market |= 1u << k;
-        type = shop_get(e, k);
-        r[2] = r[2] - (float)c_cards[type].cost;
-        e.sh[0] = (uint8_t)((e.sh[0] + 1) % 3);
-      }
-      deck(e, ag)[COG_DECK_DISCARD + type]++;
-      P.n_added_cards++;
-    } else if (a_remove) {
-      deck_remove_immediate(e, ag, (uint8_t)(a_remove - 1));
-      P.n_removes--;
-      if (!P.n_removes) enable_playing(e, ag);
-      else special = COG_SPECIAL_SHOP_OFF;
-    } else {
-      e.sh[0] = (uint8_t)((e.sh[0] + 1) % 3);
-      if (P.n_removes > 0) { P.n_removes = 0; enable_playing(e, ag); }
-    }
-    if (P.next_card_free) { P.next_card_free = 0; enable_playing(e, ag); }
-  }
-  if (P.mip && !a_move) {
-    P.mip = 0;
-    r[0] = 0.f; r[1] = 0.f; r[2] = 0.f;
-  }
-  if (P.has_won || e.sh[0] == COG_PHASE_INACTIVE) {  // maybe_end_turn / next_agent
-    end_turn(e, ag);
-    uint8_t na = (uint8_t)(pv->agent + 1);
-    if (na >= pv->n_players) na = 0;
-    pv->agent = na;
-    copy_mask(e.sel, stm(e, na));
-    r[0] = 0.f; r[1] = 0.f; r[2] = 0.f;
-    pv->turn_counter++;
-  }
-  const int cur = pv->agent;
-  update_observation(e, cur);
-  if (special != COG_SPECIAL_NONE) {
-    apply_special(e, special, ag);
-  } else {
-    const uint8_t c = lookup(e, pv->locx[cur], pv->locy[cur]);
-    if (COG_HEX_END(c) || pv->turn_counter >= pv->max_steps) finish_episode(e);
   }
 }
 
@@ -970,6 +742,10 @@ __global__ void k_init(DevState s, uint32_t default_seed) {
   z.n_players = 4; z.n_pieces = 3; z.difficulty = 0; z.max_steps = 100000;
   z.n_in_market = COG_MKT_SLOTS;
   z.in_market = kInMarket0;
+  for (int p = 0; p < 4; p++) {                            // no map yet: every lookup is outside
+    for (int d = 0; d < 7; d++) z.cells[p][d] = COG_HEX_MOUNTAIN;
+    z.cells[p][7] = 0x7f;
+  }
   *pv = z;
   uint8_t *ob = s.obs + i * COG_OBS_BYTES;
   for (int k = 0; k < COG_N_SHOP; k++) ob[COG_OBS_SHOP + k] = COG_CARDS_PER_TYPE;
@@ -1054,34 +830,24 @@ __global__ void __launch_bounds__(256) k_encode_lds(const uint8_t *__restrict__ 
   }
 }
 
-// ---- per-work-item LDS staging of a step's working set -------------------------------------
-// slot = 145 dwords (odd stride: same-offset dword accesses of a wave are bank-conflict free)
-//   [  0,128) EnvPriv line            [128,224) selected ActionMask (96 B)
-//   [224,272) ObsData 16128..16175 (phase, resources, shop)
-//   [272,384) DeckObs of the acting player a0 (112 B)   [384,480) stored ActionMask of a0
-//   [480,576) stored ActionMask of the next player na (prefetched for the turn change)
-constexpr int kSlotWords = 145;
-constexpr int SLOT_PV = 0, SLOT_SEL = 128, SLOT_SH = 224, SLOT_DK = 272, SLOT_ST = 384, SLOT_STN = 480;
+// ---- per-env LDS slots of a step's working set, staged by the whole wave ------------------
+// slot = 155 dwords (odd stride: same-offset dword accesses of a wave are bank-conflict free)
+//   [  0,160) EnvPriv                 [160,256) selected ActionMask (96 B)
+//   [256,304) ObsData 16128..16175 (phase, resources, shop)
+//   [304,416) DeckObs of the acting player a0 (112 B)   [416,512) stored ActionMask of a0
+//   [512,608) stored ActionMask of the next player na (the turn change reads it)
+//   [608,616) store plan: dirty 16-B granules of each staged record
+// Loads and stores are cooperative: item (env e, granule g) of a record goes to lane
+// (e * G + g) mod 64, so one instruction covers 64 / G whole records instead of 64 scattered
+// 16-B pieces; the game logic then runs one env per lane on its slot.
+constexpr int kSlotWords = 155;
+constexpr int SLOT_PV = 0, SLOT_SEL = 160, SLOT_SH = 256, SLOT_DK = 304, SLOT_ST = 416, SLOT_STN = 512,
+              SLOT_PLAN = 608;
+constexpr int kPvG = (int)sizeof(EnvPriv) / 16;          // 10 granules
+constexpr int kWaveEnvs = 64;
 
-DEV void stage_in(uint32_t *slot, int off, const uint8_t *g, int n16) {
-  const uint4 *src = reinterpret_cast<const uint4 *>(g);
-  uint32_t *dst = slot + off / 4;
-#pragma unroll
-  for (int q = 0; q < 8; q++) {
-    if (q < n16) {
-      const uint4 v = src[q];
-      dst[4 * q] = v.x; dst[4 * q + 1] = v.y; dst[4 * q + 2] = v.z; dst[4 * q + 3] = v.w;
-    }
-  }
-}
-// store the 16-B granules of a staged record whose bit is set in `dirty`
-DEV void stage_out(const uint32_t *slot, int off, uint8_t *g, int n16, uint32_t dirty = 0xffu) {
-  uint4 *dst = reinterpret_cast<uint4 *>(g);
-  const uint32_t *src = slot + off / 4;
-#pragma unroll
-  for (int q = 0; q < 8; q++)
-    if (q < n16 && ((dirty >> q) & 1u)) dst[q] = make_uint4(src[4 * q], src[4 * q + 1], src[4 * q + 2], src[4 * q + 3]);
-}
+DEV void lds_put4(uint32_t *d, const uint4 &v) { d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w; }
+DEV uint4 lds_get4(const uint32_t *d) { return make_uint4(d[0], d[1], d[2], d[3]); }
 
 // ---- fast path: play / pass / turn change on registers (environment.cpp:91-250) -------------
 // Selected and stored masks are held as five head bitsets (bit k == index k of the head); the
@@ -1233,38 +999,16 @@ DEV void put_move_shop(uint32_t *st32, uint32_t move, uint32_t shop) {
   for (int q = 0; q < 6; q++) st32[17 + q] = expand4((v >> (2 + 4 * q)) & 0xfu);
 }
 
-struct Cells {                        // own cell [0] and neighbours [1..6] of one player
-  uint8_t c[7];
-  uint8_t oob;                        // bit d: lookup d fell outside the map (flag only if used)
-};
-DEV Cells prefetch_cells(const Ctx &e, int player) {      // Map::get_from_array, no side effects
-  const EnvPriv *pv = e.pv;
-  Cells r;
-  r.oob = 0;
-  const int lx = pv->locx[player], ly = pv->locy[player];
-#pragma unroll
-  for (int d = 0; d < 7; d++) {
-    const int ix = lx + c_dirs[d][0] / 2 - pv->minx + 1, iy = ly + c_dirs[d][1] / 2 - pv->miny + 1;
-    const bool out = ix < 0 || iy < 0 || ix >= pv->dimx || iy >= pv->dimy;
-    const bool ring = ix >= COG_GRID || iy >= COG_GRID;
-    const int cx = min(max(ix, 0), COG_GRID - 1), cy = min(max(iy, 0), COG_GRID - 1);
-    const uint8_t v = e.cgrid[cx * COG_GRID + cy];
-    r.c[d] = (out || ring || !v) ? (uint8_t)COG_HEX_MOUNTAIN : v;
-    r.oob |= (uint8_t)((out ? 1u : 0u) << d);
-  }
-  return r;
+DEV uint8_t use_cell(const Ctx &e, const uint8_t *cc, int d) {   // a lookup of the cached cell d
+  if ((cc[7] >> d) & 1u) e.pv->flags |= F_OOB_LOOKUP;
+  return cc[d];
 }
-DEV uint8_t use_cell(const Ctx &e, const Cells &c, int d) {
-  if ((c.oob >> d) & 1u) e.pv->flags |= F_OOB_LOOKUP;
-  return c.c[d];
-}
-
-// movement mask bits 1..6 (map.cpp:369-387) + bit 0
-DEV uint32_t move_bits(const Ctx &e, const Cells &cl, float r0, float r1, float r2, uint8_t n_active) {
+// movement mask bits 1..6 (map.cpp:369-387) + bit 0, from a player's cached neighbourhood
+DEV uint32_t move_bits(const Ctx &e, const uint8_t *cc, float r0, float r1, float r2, uint8_t n_active) {
   uint32_t m = 1u;
 #pragma unroll
   for (int d = 1; d < 7; d++) {
-    const uint8_t c = use_cell(e, cl, d);
+    const uint8_t c = use_cell(e, cc, d);
     const int req = COG_HEX_REQ(c);
     const uint32_t n = COG_HEX_N(c);
     const float r = req == 0 ? r0 : (req == 1 ? r1 : r2);
@@ -1285,61 +1029,228 @@ DEV uint32_t shop_bits(const Ctx &e, float coins) {
   }
   return m;
 }
+DEV uint32_t gran(int byte) { return 1u << (byte >> 4); }   // 16-B granule bit of a record byte
 
-struct FastOut {
-  bool turn_end;
-  uint32_t dirty_dk, dirty_st;        // 16-B granules of the staged deck / stored mask of a0
+// Player::cards_from_active (player.cpp:85-131): n random cards leave the active pile
+DEV void take_from_active(const Ctx &e, PlayerPriv &P, uint8_t n, bool discard) {
+  uint8_t *d = e.dka;
+  const uint8_t avail = P.n_active;
+  if (n > avail) {
+    if (discard) e.pv->flags |= F_Q24_CLAMP;
+    n = avail;
+  }
+  uint32_t rng = e.pv->rng;
+  for (uint8_t i = 0; i < n; i++) {
+    const uint32_t t = uid(rng, (uint32_t)(avail - i));
+    const int c = scan(e, d, COG_DECK_ACTIVE, t);
+    P.n_active--;
+    d[COG_DECK_ACTIVE + c]--;
+    if (discard) d[COG_DECK_DISCARD + c]++;
+  }
+  e.pv->rng = rng;
+}
+
+// card c leaves the hand (Deck::activate / play_immediate / remove_immediate, cards.cpp:242-290)
+// and the selected mask's play / special / remove bits of c follow (rem_rule: remove_immediate)
+DEV void leave_hand(const Ctx &e, PlayerPriv &P, Heads &sel, int c, bool rem_rule) {
+  const uint8_t prev = e.dka[COG_DECK_HAND + c];
+  e.dka[COG_DECK_HAND + c] = (uint8_t)(prev - 1);
+  P.n_in_hand--;
+  const uint32_t b = 1u << (c + 1);
+  bool pl = prev > 1;
+  if (rem_rule) {
+    if (!pl) sel.rem &= ~b;
+    pl = pl && (sel.play & b);
+  }
+  sel.play = pl ? (sel.play | b) : (sel.play & ~b);
+  sel.spec = (pl && is_special(c)) ? (sel.spec | b) : (sel.spec & ~b);
+}
+
+struct Plan {                         // 16-B granules to store back, per staged record
+  uint32_t pv, sh, dk, st, stn;
 };
 
-// cog_env::step for play / pass actions (environment.cpp:91-107, 128-150 pass branch, 176-207)
-DEV FastOut fast_step(const Ctx &e, const uint8_t act[5], Heads &sel, uint8_t *stn, const Cells cl[2], int na) {
-  FastOut o{false, 0u, 0u};
+// special actions (cards.cpp:8-36, the remove lambda environment.cpp:156-158) on the stored mask
+// `stc` of the CURRENT agent and the selected mask, for the ACTING player P (:183-186)
+DEV void apply_special(const Ctx &e, int special, int ag, PlayerPriv &P, Heads &sel, uint8_t *stc) {
+  Heads m = heads_from(stc);
+  switch (special) {
+    case COG_SPECIAL_DRAW2:
+    case COG_SPECIAL_DRAW3: {
+      uint32_t rng = e.pv->rng;
+      fast_draw(e, P, reinterpret_cast<uint32_t *>(e.dka), sel, rng, special == COG_SPECIAL_DRAW2 ? 2 : 3);
+      e.pv->rng = rng;
+    } break;
+    case COG_SPECIAL_DRAW1_REMOVE1:
+    case COG_SPECIAL_DRAW2_REMOVE2: {
+      const uint8_t k = special == COG_SPECIAL_DRAW1_REMOVE1 ? 1 : 2;
+      uint32_t rng = e.pv->rng;
+      fast_draw(e, P, reinterpret_cast<uint32_t *>(e.dka), sel, rng, k);
+      e.pv->rng = rng;
+      P.n_removes = k;
+      m.rem = m.play;                                      // mask.remove = mask.play
+      sel.play = 1u;                                       // disable_playing
+      sel.spec = 1u;
+      m.shop &= 1u;                                        // shop_mask(0): nothing affordable
+    } break;
+    case COG_SPECIAL_TRANSMIT: {
+      m.move = 1u;
+      sel.play = 1u;
+      sel.spec = 1u;
+      uint32_t sb = m.shop & 1u;
+#pragma unroll
+      for (int i = 0; i < COG_N_SHOP; i++)
+        if (e.sh[SH_SHOP + i] > 0) sb |= 1u << (i + 1);
+      m.shop = sb;
+      P.next_card_free = 1;
+    } break;
+    case COG_SPECIAL_NATIVE: {
+      const uint8_t *cc = e.pv->cells[ag];
+      uint32_t mb = m.move & 1u;
+#pragma unroll
+      for (int d = 1; d < 7; d++)                          // movement_mask with 100 of everything
+        if (COG_HEX_REQ(use_cell(e, cc, d)) != COG_REQ_NULL) mb |= 1u << d;
+      m.move = mb;
+      P.next_move_free = 1;
+      sel.play = 1u;
+      sel.spec = 1u;
+      m.shop &= 1u;
+    } break;
+    case COG_SPECIAL_SHOP_OFF: m.shop &= 1u; break;
+    default: break;
+  }
+  heads_to(m, reinterpret_cast<uint32_t *>(stc));
+}
+
+// cog_env::step (environment.cpp:91-224) for the acting player a0 == agent, every action kind.
+// State: deck / stored mask of a0, stored mask of na, phase / resources / shop and EnvPriv in
+// the LDS slot; selected mask in `sel` (bitsets).  Returns the granules it modified.
+DEV Plan step_env(const Ctx &e, const uint8_t act[5], Heads &sel, uint8_t *stn, int na) {
   EnvPriv *pv = e.pv;
   const int ag = pv->agent;
+  Plan o{0xbu | (1u << (4 + ag)), 0x1u, 0u, 0u, 0u};       // rng/counters, agent/flags, info mirror
+  e.info[COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag] = ++pv->info_steps[ag];   // steps_taken (u8)
   uint8_t phase = e.sh[0];
   if (phase == COG_PHASE_INACTIVE) phase = COG_PHASE_MOVEMENT;
   PlayerPriv &P = pv->pl[ag];
   P.steps_taken++;
   float *res3 = res(e);
   float r0 = res3[0], r1 = res3[1], r2 = res3[2];
-  uint32_t *dk32 = reinterpret_cast<uint32_t *>(e.dka);
-  if (act[0]) {                                            // Player::play_card + Deck::activate
-    const int c = (uint8_t)(act[0] - 1);
+  uint8_t *d = e.dka;
+  uint32_t *dk32 = reinterpret_cast<uint32_t *>(d);
+  const uint8_t a_play = act[0], a_special = act[1], a_remove = act[2], a_move = act[3], a_shop = act[4];
+  int special = COG_SPECIAL_NONE;
+  bool moved = false;
+  if (a_play) {                                            // Player::play_card (player.cpp:45-60)
+    const int c = a_play - 1;
     if (phase == COG_PHASE_MOVEMENT) {
       r0 = (float)c_cards[c].res[0]; r1 = (float)c_cards[c].res[1]; r2 = (float)c_cards[c].res[2];
     } else if (phase == COG_PHASE_BUYING) {
       const uint8_t coin = c_cards[c].res[2];
       r2 = r2 + (coin > 0 ? (float)coin : 0.5f);
     }
-    P.n_in_hand--;
+    leave_hand(e, P, sel, c, false);                       // Deck::activate
+    d[COG_DECK_ACTIVE + c]++;
     P.n_active++;
     P.idx_last = (uint8_t)c;
-    const uint8_t prev = e.dka[COG_DECK_HAND + c];
-    e.dka[COG_DECK_HAND + c] = (uint8_t)(prev - 1);
-    e.dka[COG_DECK_ACTIVE + c]++;
-    const bool pl = prev > 1;
-    sel.play = set_bit(sel.play, c + 1, pl);
-    sel.spec = set_bit(sel.spec, c + 1, pl && is_special(c));
-    o.dirty_dk |= (1u << ((COG_DECK_HAND + c) >> 4)) | (1u << ((COG_DECK_ACTIVE + c) >> 4));
-  } else {                                                 // pass
-    P.next_move_free = 0;
-    phase = (uint8_t)((phase + 1) % 3);
-    if (P.n_removes > 0) {
-      P.n_removes = 0;
+    o.dk |= gran(COG_DECK_HAND + c) | gran(COG_DECK_ACTIVE + c);
+  } else if (a_special) {                                  // play_special (environment.cpp:108-114)
+    const int c = a_special - 1;
+    const bool single = c_cards[c].single_use;
+    leave_hand(e, P, sel, c, single);                      // remove_immediate / play_immediate
+    if (!single) {
+      d[COG_DECK_PLAYED + c]++;
+      o.dk |= gran(COG_DECK_PLAYED + c);
+    }
+    o.dk |= gran(COG_DECK_HAND + c);
+    special = c_cards[c].special;
+  } else if (a_move) {                                     // move (environment.cpp:115-127)
+    const uint8_t c = use_cell(e, pv->cells[ag], a_move);
+    pv->locx[ag] = (int8_t)(pv->locx[ag] + c_dirs[a_move][0] / 2);
+    pv->locy[ag] = (int8_t)(pv->locy[ag] + c_dirs[a_move][1] / 2);
+    if (!P.next_move_free) {                               // Player::handle_requirement (:141-162)
+      const int req = COG_HEX_REQ(c);
+      const uint8_t n = COG_HEX_N(c);
+      if (req < 3) {
+        const float left = (req == 0 ? r0 : req == 1 ? r1 : r2) - (float)n;
+        r0 = req == 0 ? left : 0.f;
+        r1 = req == 1 ? left : 0.f;
+        r2 = req == 2 ? left : 0.f;
+        if (!P.mip) {                                      // Deck::play_last_activated
+          const int l = P.idx_last;
+          P.n_active--;
+          d[COG_DECK_ACTIVE + l]--;
+          o.dk |= gran(COG_DECK_ACTIVE + l);
+          if (!c_cards[l].single_use) {
+            d[COG_DECK_PLAYED + l]++;
+            o.dk |= gran(COG_DECK_PLAYED + l);
+          }
+          P.mip = 1;
+        }
+      } else if (req == COG_REQ_REMOVE || req == COG_REQ_DISCARD) {
+        take_from_active(e, P, n, req == COG_REQ_DISCARD);
+        r0 = r1 = r2 = 0.f;
+        P.mip = 0;
+        o.dk = 0x7fu;
+      }
+    } else {
+      P.next_move_free = 0;
       fast_enable_playing(dk32, sel);
+    }
+    P.n_movements++;
+    P.has_won = COG_HEX_END(c);
+    moved = true;
+    o.pv |= 0x4u;                                          // player locations
+  } else {
+    P.next_move_free = 0;
+    if (a_shop) {                                          // Shop::get_card (cards.cpp:123-142)
+      const int k = a_shop - 1;
+      const int type = kShopTypes[k];
+      const uint32_t bit = 1u << k;
+      if (!P.next_card_free) {
+        pv->n_in_market = (uint8_t)(pv->n_in_market + ((pv->in_market & bit) ? 0 : 1));
+        pv->in_market |= bit;
+      }
+      const uint8_t left = (uint8_t)(e.sh[SH_SHOP + k] - 1);
+      e.sh[SH_SHOP + k] = left;
+      if (!left && (pv->in_market & bit)) {
+        pv->in_market &= ~bit;
+        pv->n_in_market--;
+      }
+      if (!P.next_card_free) {
+        r2 = r2 - (float)c_cards[type].cost;
+        phase = (uint8_t)((phase + 1) % 3);
+      }
+      d[COG_DECK_DISCARD + type]++;
+      P.n_added_cards++;
+      o.dk |= gran(COG_DECK_DISCARD + type);
+      o.sh |= gran(SH_SHOP + k);
+    } else if (a_remove) {
+      const int c = a_remove - 1;
+      leave_hand(e, P, sel, c, true);                      // Deck::remove_immediate
+      o.dk |= gran(COG_DECK_HAND + c);
+      P.n_removes--;
+      if (!P.n_removes) fast_enable_playing(dk32, sel);
+      else special = COG_SPECIAL_SHOP_OFF;
+    } else {                                               // pass: next phase
+      phase = (uint8_t)((phase + 1) % 3);
+      if (P.n_removes > 0) {
+        P.n_removes = 0;
+        fast_enable_playing(dk32, sel);
+      }
     }
     if (P.next_card_free) {
       P.next_card_free = 0;
       fast_enable_playing(dk32, sel);
     }
   }
-  if (P.mip && !act[3]) {                                  // the move HEAD, even when play won
+  STAMP_AT(3);
+  if (P.mip && !a_move) {                                  // the move HEAD, whatever was taken
     P.mip = 0;
     r0 = r1 = r2 = 0.f;
   }
   int cur = ag;
   if (P.has_won || phase == COG_PHASE_INACTIVE) {          // maybe_end_turn -> next_agent
-    o.turn_end = true;
     P.n_active = 0;                                        // Player::end_turn (player.cpp:170-180)
     fast_discard_all(dk32);
     const int n_draw = COG_HAND_SIZE - (int)P.n_in_hand;
@@ -1349,144 +1260,238 @@ DEV FastOut fast_step(const Ctx &e, const uint8_t act[5], Heads &sel, uint8_t *s
       pv->rng = rng;
     }
     heads_to(sel, reinterpret_cast<uint32_t *>(e.sta));  // save_actionmask
-    o.dirty_dk = 0x7fu;
-    o.dirty_st = 0x3fu;
+    o.dk = 0x7fu;
+    o.st = 0x3fu;
     pv->agent = (uint8_t)na;
     sel = heads_from(na == ag ? e.sta : stn);             // load_actionmask
     r0 = r1 = r2 = 0.f;
     pv->turn_counter++;
     cur = na;
   }
+  STAMP_AT(4);
   e.sh[0] = phase;
   res3[0] = r0; res3[1] = r1; res3[2] = r2;
-  const Cells &cc = cur == ag ? cl[0] : cl[1];
+  if (moved) {                                             // the mover's new neighbourhood
+    load_cells(e, ag);
+    o.pv |= 1u << (8 + ag / 2);
+  }
+  STAMP_AT(5);
+  const uint8_t *cc = pv->cells[cur];
+  uint8_t *stc = cur == ag ? e.sta : stn;
   uint32_t mv = 1u, sp = 1u;                               // update_observation (:252-279)
   if (phase == COG_PHASE_MOVEMENT) mv = move_bits(e, cc, r0, r1, r2, pv->pl[cur].n_active);
   else if (phase == COG_PHASE_BUYING) sp = shop_bits(e, r2);
-  if (cur == ag) {
-    put_move_shop(reinterpret_cast<uint32_t *>(e.sta), mv, sp);
-    o.dirty_st |= 0x30u;
+  put_move_shop(reinterpret_cast<uint32_t *>(stc), mv, sp);
+  STAMP_AT(6);
+  uint32_t st_dirty = 0x30u;
+  if (special != COG_SPECIAL_NONE) {
+    apply_special(e, special, ag, P, sel, stc);
+    st_dirty = 0x3fu;
+    o.dk = 0x7fu;
   } else {
-    put_move_shop(reinterpret_cast<uint32_t *>(stn), mv, sp);
+    const uint8_t c = use_cell(e, cc, 0);                  // done check (:187)
+    if (COG_HEX_END(c) || pv->turn_counter >= pv->max_steps) finish_episode(e);
   }
-  const uint8_t c = use_cell(e, cc, 0);                    // done check (:187)
-  if (COG_HEX_END(c) || pv->turn_counter >= pv->max_steps) finish_episode(e);
+  STAMP_AT(7);
+  if (cur == ag) o.st |= st_dirty;
+  else o.stn |= st_dirty;
   return o;
 }
 
-// One env step (optionally preceded by sampling its action), state staged through LDS.
+// One step of the wave's 64 envs (each optionally preceded by sampling its action).
 // act_in: actions of the host API path (nullptr in the fused runner path).
-DEV void staged_step(const DevState &s, uint32_t *slot, size_t i, const uint8_t *act_in, int mask_source,
-                     uint32_t *rngs, uint8_t *actions_out, bool &enc) {
+DEV void wave_step(const DevState &s, uint32_t *slots, const uint8_t *act_in, int mask_source,
+                   uint32_t *rngs, uint8_t *actions_out) {
+  const int lane = threadIdx.x;
+  const size_t base = (size_t)blockIdx.x * kWaveEnvs;
+  const int nv = s.n - base < (size_t)kWaveEnvs ? (int)(s.n - base) : kWaveEnvs;
+  auto slot_of = [&](int e) { return slots + e * kSlotWords; };
+  auto pv_of = [&](int e) { return reinterpret_cast<const EnvPriv *>(slot_of(e) + SLOT_PV / 4); };
+  auto obs_of = [&](int e) { return s.obs + (base + e) * COG_OBS_BYTES; };
+  auto player_of = [&](int e, int p) { return obs_of(e) + COG_OBS_PLAYER0 + COG_OBS_PLAYER_STRIDE * p; };
   STAMP(s, 0);
-  uint8_t *ob = s.obs + i * COG_OBS_BYTES;
-  uint8_t *gsel = s.sel + i * COG_MASK_BYTES;
-  uint8_t *gpv = reinterpret_cast<uint8_t *>(s.priv + i);
-  stage_in(slot, SLOT_PV, gpv, 8);
-  stage_in(slot, SLOT_SEL, gsel, 6);
-  stage_in(slot, SLOT_SH, ob + COG_OBS_PHASE, 3);
-  uint8_t *lds = reinterpret_cast<uint8_t *>(slot);
-  EnvPriv *pv = reinterpret_cast<EnvPriv *>(lds + SLOT_PV);
-  const int a0 = pv->agent;
-  const int na = a0 + 1 >= pv->n_players ? 0 : a0 + 1;
-  uint8_t *gdk = ob + COG_OBS_PLAYER0 + COG_OBS_PLAYER_STRIDE * a0;
-  uint8_t *gstn = ob + COG_OBS_PLAYER0 + COG_OBS_PLAYER_STRIDE * na + COG_PD_MASK;
-  stage_in(slot, SLOT_DK, gdk, 7);
-  stage_in(slot, SLOT_ST, gdk + COG_PD_MASK, 6);
-  stage_in(slot, SLOT_STN, gstn, 6);
 
-  Ctx e;
-  e.ob = ob;
-  e.sh = lds + SLOT_SH;
-  e.dka = lds + SLOT_DK;
-  e.sta = lds + SLOT_ST;
-  e.a0 = a0;
-  e.sel = lds + SLOT_SEL;
-  e.info = s.info + i * COG_INFO_BYTES;
-  e.rew = s.rew + i * 4;
-  e.pv = pv;
-  e.grid = s.grid + i * (size_t)kGridBytes;
-  e.cgrid = s.cgrid + i * COG_CELLS;
-  e.gs = s.gen + i;
-  Cells cl[2];
-  cl[0] = prefetch_cells(e, a0);
-  cl[1] = prefetch_cells(e, na);
-  uint8_t *ginfo_steps = e.info + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * a0;
-  const uint8_t info_steps = *ginfo_steps;
-  STAMP(s, 1);
-
-  Heads sel = heads_from(e.sel);
-  uint8_t act[5];
-  if (act_in) {
-    for (int k = 0; k < 5; k++) act[k] = act_in[k];
-  } else {                                                 // runner: sample(selected | stored mask)
-    uint32_t rng = rngs[i];
-    if (mask_source == MASK_STORED) sample_heads(heads_from(e.sta), rng, act);
-    else sample_heads(sel, rng, act);
-    rngs[i] = rng;
-    store_action(actions_out + i * COG_ACTION_BYTES, act);
-  }
-  STAMP(s, 2);
-  const bool fast = !pv->done && (act[0] != 0 || (act[1] == 0 && act[2] == 0 && act[3] == 0 && act[4] == 0));
-  FastOut fo{false, 0x7fu, 0x3fu};
-  uint32_t dirty_pv = 0xffu, dirty_sh = 0x7u;
-  bool sel_in_regs = false;
-  if (fast) {
-    *ginfo_steps = (uint8_t)(info_steps + 1);              // agent_infos[a].steps_taken += 1
-    fo = fast_step(e, act, sel, lds + SLOT_STN, cl, na);
-    sel_in_regs = true;
-    dirty_pv = 0x3u | (1u << (4 + a0));
-    dirty_sh = 0x1u;
-  } else {
-    env_step(e, act);
-  }
-  STAMP(s, 3);
-  const uint8_t done = pv->done;
-  s.done[i] = done;                                        // dones[i] before the auto-reset
-  if (fast && fo.turn_end && na != a0)                      // next player's refreshed move / shop bytes
-    stage_out(slot, SLOT_STN, gstn, 6, 0x30u);
-  if (done) {                                              // vec_environment.h:56-59
-    if (sel_in_regs) heads_to(sel, reinterpret_cast<uint32_t *>(e.sel));
-    sel_in_regs = false;
-    fo.dirty_dk = 0x7fu;
-    fo.dirty_st = 0x3fu;
-    dirty_pv = 0xffu;
-    dirty_sh = 0x7u;
-    if (!env_reset(e)) {
-      atomicOr(&s.status[0], pv->flags);
-      atomicAdd(&s.status[1], 1u);
-    } else {
-      enc = true;
-      const uint32_t k = atomicAdd(&s.status[2], 1u);
-      if (k < s.n) s.dirty[k] = (uint32_t)i;
+  // round 1: EnvPriv (10 granules), selected mask (6), phase/resources/shop (3)
+  {
+    uint4 a[kPvG], b[6], c[3];
+#pragma unroll
+    for (int k = 0; k < kPvG; k++) {
+      const int it = k * 64 + lane, e = it / kPvG, g = it % kPvG;
+      if (e < nv) a[k] = reinterpret_cast<const uint4 *>(s.priv + base + e)[g];
+    }
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      const int it = k * 64 + lane, e = it / 6, g = it % 6;
+      if (e < nv) b[k] = reinterpret_cast<const uint4 *>(s.sel + (base + e) * COG_MASK_BYTES)[g];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const int it = k * 64 + lane, e = it / 3, g = it % 3;
+      if (e < nv) c[k] = reinterpret_cast<const uint4 *>(obs_of(e) + COG_OBS_PHASE)[g];
+    }
+#pragma unroll
+    for (int k = 0; k < kPvG; k++) {
+      const int it = k * 64 + lane, e = it / kPvG, g = it % kPvG;
+      if (e < nv) lds_put4(slot_of(e) + SLOT_PV / 4 + 4 * g, a[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      const int it = k * 64 + lane, e = it / 6, g = it % 6;
+      if (e < nv) lds_put4(slot_of(e) + SLOT_SEL / 4 + 4 * g, b[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const int it = k * 64 + lane, e = it / 3, g = it % 3;
+      if (e < nv) lds_put4(slot_of(e) + SLOT_SH / 4 + 4 * g, c[k]);
     }
   }
-  s.agent[i] = pv->agent;
-  STAMP(s, 4);
-  if (sel_in_regs) {
-    uint32_t m[24];
-    heads_to(sel, m);
-    m[23] = 0u;
-    uint4 *d = reinterpret_cast<uint4 *>(gsel);
+  __syncthreads();
+
+  // round 2 (addresses depend on the agent): deck + stored mask of a0 (13 granules, skipping
+  // the DeckObs padding granule), stored mask of na (6)
+  {
+    uint4 a[13], b[6];
 #pragma unroll
-    for (int q = 0; q < 6; q++) d[q] = make_uint4(m[4 * q], m[4 * q + 1], m[4 * q + 2], m[4 * q + 3]);
-  } else {
-    stage_out(slot, SLOT_SEL, gsel, 6);
+    for (int k = 0; k < 13; k++) {
+      const int it = k * 64 + lane, e = it / 13, g = it % 13;
+      if (e < nv) a[k] = reinterpret_cast<const uint4 *>(player_of(e, pv_of(e)->agent))[g < 7 ? g : g + 1];
+    }
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      const int it = k * 64 + lane, e = it / 6, g = it % 6;
+      if (e < nv) {
+        const EnvPriv *pv = pv_of(e);
+        const int na = pv->agent + 1 >= pv->n_players ? 0 : pv->agent + 1;
+        b[k] = reinterpret_cast<const uint4 *>(player_of(e, na) + COG_PD_MASK)[g];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 13; k++) {
+      const int it = k * 64 + lane, e = it / 13, g = it % 13;
+      if (e < nv) lds_put4(slot_of(e) + SLOT_DK / 4 + 4 * g, a[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      const int it = k * 64 + lane, e = it / 6, g = it % 6;
+      if (e < nv) lds_put4(slot_of(e) + SLOT_STN / 4 + 4 * g, b[k]);
+    }
   }
-  stage_out(slot, SLOT_PV, gpv, 8, dirty_pv);
-  stage_out(slot, SLOT_SH, ob + COG_OBS_PHASE, 3, dirty_sh);
-  stage_out(slot, SLOT_DK, gdk, 7, fo.dirty_dk);
-  stage_out(slot, SLOT_ST, gdk + COG_PD_MASK, 6, fo.dirty_st);
-  STAMP(s, 5);
+  __syncthreads();
+  STAMP(s, 1);
+
+  // per-lane game logic on the slot of env `lane`
+  const size_t i = base + lane;
+  bool enc = false;
+  if (lane < nv) {
+    uint32_t *slot = slot_of(lane);
+    uint8_t *lds = reinterpret_cast<uint8_t *>(slot);
+    EnvPriv *pv = reinterpret_cast<EnvPriv *>(lds + SLOT_PV);
+    const int a0 = pv->agent;
+    const int na = a0 + 1 >= pv->n_players ? 0 : a0 + 1;
+    Ctx e;
+    e.ob = s.obs + i * COG_OBS_BYTES;
+    e.sh = lds + SLOT_SH;
+    e.dka = lds + SLOT_DK;
+    e.sta = lds + SLOT_ST;
+    e.a0 = a0;
+    e.sel = lds + SLOT_SEL;
+    e.info = s.info + i * COG_INFO_BYTES;
+    e.rew = s.rew + i * 4;
+    e.pv = pv;
+    e.grid = s.grid + i * (size_t)kGridBytes;
+    e.cgrid = s.cgrid + i * COG_CELLS;
+    e.gs = s.gen + i;
+    e.stamps = s.stamps;
+
+    Heads sel = heads_from(e.sel);
+    uint8_t act[5];
+    if (act_in) {                                          // host actions: indices past a head
+      const uint8_t *ai = act_in + i * COG_ACTION_BYTES;   // are the reference's OOB accesses
+      const uint8_t top[5] = {COG_N_CARDTYPES, COG_N_CARDTYPES, COG_N_CARDTYPES, 6, COG_N_SHOP};
+      for (int k = 0; k < 5; k++) {
+        act[k] = ai[k];
+        if (act[k] > top[k]) {
+          act[k] = top[k];
+          pv->flags |= F_BAD_ACTION;
+        }
+      }
+    } else {                                               // runner: sample(selected | stored mask)
+      uint32_t rng = rngs[i];
+      if (mask_source == MASK_STORED) sample_heads(heads_from(e.sta), rng, act);
+      else sample_heads(sel, rng, act);
+      rngs[i] = rng;
+      store_action(actions_out + i * COG_ACTION_BYTES, act);
+    }
+    STAMP(s, 2);
+    Plan o{0x3u, 0u, 0u, 0u, 0u};                          // flags may change (bad action)
+    if (!pv->done) o = step_env(e, act, sel, lds + SLOT_STN, na);
+    STAMP(s, 10);
+    const uint8_t done = pv->done;
+    s.done[i] = done;                                      // dones[i] before the auto-reset
+    if (done) {                                            // vec_environment.h:56-59
+      heads_to(sel, reinterpret_cast<uint32_t *>(e.sel));
+      o = Plan{(1u << kPvG) - 1u, 0x7u, 0x7fu, 0x3fu, 0u}; // na's staged mask is stale now
+      if (!env_reset(e)) {
+        atomicOr(&s.status[0], pv->flags);
+        atomicAdd(&s.status[1], 1u);
+      } else {
+        enc = true;
+        const uint32_t k = atomicAdd(&s.status[2], 1u);
+        if (k < s.n) s.dirty[k] = (uint32_t)i;
+      }
+      sel = heads_from(e.sel);
+    }
+    s.agent[i] = pv->agent;
+    heads_to(sel, slot + SLOT_SEL / 4);
+    slot[SLOT_PLAN / 4] = o.pv | o.sh << 10 | o.dk << 13 | o.st << 20 | o.stn << 26;
+    slot[SLOT_PLAN / 4 + 1] = (uint32_t)a0 | (uint32_t)na << 2;   // records of the ORIGINAL agent
+    STAMP(s, 11);
+  }
+  __syncthreads();
+
+  // cooperative stores of the dirty granules
+#pragma unroll
+  for (int k = 0; k < kPvG; k++) {
+    const int it = k * 64 + lane, e = it / kPvG, g = it % kPvG;
+    if (e < nv && ((slot_of(e)[SLOT_PLAN / 4] >> g) & 1u))
+      reinterpret_cast<uint4 *>(s.priv + base + e)[g] = lds_get4(slot_of(e) + SLOT_PV / 4 + 4 * g);
+  }
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    const int it = k * 64 + lane, e = it / 6, g = it % 6;
+    if (e < nv) reinterpret_cast<uint4 *>(s.sel + (base + e) * COG_MASK_BYTES)[g] = lds_get4(slot_of(e) + SLOT_SEL / 4 + 4 * g);
+  }
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const int it = k * 64 + lane, e = it / 3, g = it % 3;
+    if (e < nv && ((slot_of(e)[SLOT_PLAN / 4] >> (10 + g)) & 1u))
+      reinterpret_cast<uint4 *>(obs_of(e) + COG_OBS_PHASE)[g] = lds_get4(slot_of(e) + SLOT_SH / 4 + 4 * g);
+  }
+#pragma unroll
+  for (int k = 0; k < 13; k++) {                           // deck granules = plan bits 13..19,
+    const int it = k * 64 + lane, e = it / 13, g = it % 13; // stored-mask granules = bits 20..25
+    const uint32_t plan = e < nv ? slot_of(e)[SLOT_PLAN / 4] : 0u;
+    if ((plan >> (13 + g)) & 1u) {
+      uint8_t *p = player_of(e, slot_of(e)[SLOT_PLAN / 4 + 1] & 3u);
+      reinterpret_cast<uint4 *>(p)[g < 7 ? g : g + 1] = lds_get4(slot_of(e) + SLOT_DK / 4 + 4 * g);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 6; k++) {                            // na's stored mask = bits 26..31
+    const int it = k * 64 + lane, e = it / 6, g = it % 6;
+    const uint32_t plan = e < nv ? slot_of(e)[SLOT_PLAN / 4] : 0u;
+    if ((plan >> (26 + g)) & 1u) {
+      uint8_t *p = player_of(e, (slot_of(e)[SLOT_PLAN / 4 + 1] >> 2) & 3u) + COG_PD_MASK;
+      reinterpret_cast<uint4 *>(p)[g] = lds_get4(slot_of(e) + SLOT_STN / 4 + 4 * g);
+    }
+  }
+  STAMP(s, 12);
+  wave_encode(s, i, enc);
 }
 
-__global__ void __launch_bounds__(256) k_step(DevState s, const uint8_t *__restrict__ actions) {
-  __shared__ uint32_t slots[256 * kSlotWords];
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool enc = false;
-  if (i < s.n)
-    staged_step(s, slots + threadIdx.x * kSlotWords, i, actions + i * COG_ACTION_BYTES, 0, nullptr, nullptr, enc);
-  wave_encode(s, i, enc);
+__global__ void __launch_bounds__(64) k_step(DevState s, const uint8_t *__restrict__ actions) {
+  __shared__ uint32_t slots[kWaveEnvs * kSlotWords];
+  wave_step(s, slots, actions, 0, nullptr, nullptr);
 }
 
 __global__ void __launch_bounds__(256) k_sample(size_t n, const uint8_t *__restrict__ masks,
@@ -1500,13 +1505,10 @@ __global__ void __launch_bounds__(256) k_sample(size_t n, const uint8_t *__restr
   store_action(actions + i * COG_ACTION_BYTES, a);
 }
 
-__global__ void __launch_bounds__(256) k_sample_step(DevState s, int mask_source, uint32_t *__restrict__ rngs,
-                                                     uint8_t *__restrict__ actions) {
-  __shared__ uint32_t slots[256 * kSlotWords];
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool enc = false;
-  if (i < s.n) staged_step(s, slots + threadIdx.x * kSlotWords, i, nullptr, mask_source, rngs, actions, enc);
-  wave_encode(s, i, enc);
+__global__ void __launch_bounds__(64) k_sample_step(DevState s, int mask_source, uint32_t *__restrict__ rngs,
+                                                    uint8_t *__restrict__ actions) {
+  __shared__ uint32_t slots[kWaveEnvs * kSlotWords];
+  wave_step(s, slots, nullptr, mask_source, rngs, actions);
 }
 
 __global__ void k_seed_sampler(size_t n, uint32_t seed, uint32_t *rngs) {
@@ -1542,7 +1544,7 @@ int launch_encode_all(const DevState &s, void *stream, int variant) {
 }
 int launch_step(const DevState &s, const uint8_t *d_actions, void *stream) {
   if (!s.n) return 0;
-  hipLaunchKernelGGL(k_step, dim3(blocks_for(s.n, 256)), dim3(256), 0, (hipStream_t)stream, s, d_actions);
+  hipLaunchKernelGGL(k_step, dim3(blocks_for(s.n, kWaveEnvs)), dim3(kWaveEnvs), 0, (hipStream_t)stream, s, d_actions);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_sample(size_t n, const uint8_t *d_masks, uint32_t *d_rng, uint8_t *d_actions, void *stream) {
@@ -1552,7 +1554,7 @@ int launch_sample(size_t n, const uint8_t *d_masks, uint32_t *d_rng, uint8_t *d_
 }
 int launch_sample_step(const DevState &s, int mask_source, uint32_t *d_rng, uint8_t *d_actions, void *stream) {
   if (!s.n) return 0;
-  hipLaunchKernelGGL(k_sample_step, dim3(blocks_for(s.n, 256)), dim3(256), 0, (hipStream_t)stream, s,
+  hipLaunchKernelGGL(k_sample_step, dim3(blocks_for(s.n, kWaveEnvs)), dim3(kWaveEnvs), 0, (hipStream_t)stream, s,
                      mask_source, d_rng, d_actions);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -62,6 +62,7 @@ extern "C" {
 #define COG_HAZ_OOB_LOOKUP 0x20u   /* hex lookup outside the map: reads as mountain */
 #define COG_HAZ_SCAN_OVER 0x40u    /* card scan past the DeckObs record */
 #define COG_HAZ_B_START_LT4 0x80u  /* start piece B with < 4 players */
+#define COG_HAZ_BAD_ACTION 0x100u  /* host action index past its head (reference: OOB access): clamped */
 
 /* runner flags */
 #define COG_RUNNER_DEVICE_VIEWS 0x1u  /* sync() does not refresh the host views (C5: outputs stay in HBM) */

@@ -22,29 +22,42 @@ int main(int argc, char **argv) {
   cog_runner_rollout(run, 100);
   cog_runner_sync(run);
   const size_t waves = (n + 63) / 64;
+  constexpr int K = 16;
   unsigned long long *d;
-  hipMalloc(&d, waves * 8 * sizeof(unsigned long long));
+  if (hipMalloc(&d, waves * K * sizeof(unsigned long long)) != hipSuccess) return 1;
   env->s.stamps = d;
-  std::vector<unsigned long long> h(waves * 8);
-  std::vector<double> ph[6];
+  std::vector<unsigned long long> h(waves * K);
+  // phase j = ticks from the previous stamp that was reached to stamp j
+  const char *names[K] = {"", "stage-in (2 dependent rounds, cooperative)", "sample (5 masked picks)",
+                          "step: action branch", "step: mip + turn end (discard, draw)",
+                          "step: mover's cell reload", "step: update_observation masks",
+                          "step: special / done check", "", "", "step: rest", "auto-reset + plan",
+                          "cooperative stores issued", "", "", ""};
+  std::vector<double> ph[K], tot;
   for (int t = 0; t < steps; t++) {
-    hipMemset(d, 0, waves * 8 * sizeof(unsigned long long));
+    if (hipMemset(d, 0, waves * K * sizeof(unsigned long long)) != hipSuccess) return 1;
     cog_runner_rollout(run, 1);
     cog_runner_sync(run);
-    hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost);
+    if (hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return 1;
     for (size_t w = 0; w < waves; w++) {
-      for (int k = 1; k < 6; k++) ph[k].push_back((double)(long long)(h[w * 8 + k] - h[w * 8 + k - 1]));
-      ph[0].push_back((double)(long long)(h[w * 8 + 5] - h[w * 8 + 0]));
+      const unsigned long long *r = &h[w * K];
+      int prev = 0;
+      for (int k = 1; k < K; k++) {
+        if (!r[k]) continue;
+        ph[k].push_back((double)(long long)(r[k] - r[prev]));
+        prev = k;
+      }
+      tot.push_back((double)(long long)(r[prev] - r[0]));
     }
   }
-  const char *names[] = {"total", "stage-in (2 dependent rounds of 16-B loads)", "sample (5 masked picks)",
-                         "env_step", "auto-reset + outputs", "stage-out (stores issued)"};
-  printf("s_memtime ticks per wave, median / p90 (n=%zu, %d steps):\n", n, steps);
-  for (int k = 1; k < 7; k++) {
-    const int j = k % 6;
-    std::vector<double> &v = ph[j];
+  printf("s_memtime ticks per wave, median / p90 / max (n=%zu, %d steps):\n", n, steps);
+  for (int k = 1; k < K; k++) {
+    std::vector<double> &v = ph[k];
+    if (v.empty()) continue;
     std::sort(v.begin(), v.end());
-    printf("  %-48s %10.0f %10.0f\n", names[j], v[v.size() / 2], v[v.size() * 9 / 10]);
+    printf("  %-46s %9.0f %9.0f %9.0f  (%zu)\n", names[k], v[v.size() / 2], v[v.size() * 9 / 10], v.back(), v.size());
   }
+  std::sort(tot.begin(), tot.end());
+  printf("  %-46s %9.0f %9.0f %9.0f\n", "total", tot[tot.size() / 2], tot[tot.size() * 9 / 10], tot.back());
   return 0;
 }
