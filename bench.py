@@ -107,13 +107,16 @@ class Dist:
 
 
 def load_pmc_traffic(kernel):
-    """Per-launch HBM bytes for `kernel` measured by rocprofv3 --pmc (profiles/pmc_traffic.json)."""
+    """Per-launch HBM bytes for `kernel` measured by rocprofv3 --pmc (profiles/pmc_traffic.json,
+    written by tools/pmc_traffic.py); None unless it was measured on this exact engine source."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from pmc_traffic import engine_hash
         with open(p) as f:
             d = json.load(f)
         e = d.get(kernel)
-        if e and e.get("envs_per_launch") == N_ENVS_PER_GPU:
+        if e and e.get("envs_per_launch") == N_ENVS_PER_GPU and d.get("engine_sha") == engine_hash():
             return float(e["bytes_per_launch"])
     except Exception:
         pass
@@ -187,7 +190,8 @@ def main():
     total_env_steps = d.sum(float(n) * args.steps)
     value = total_env_steps / wall_max
 
-    # ---- kernel timing for the roofline (separate pass, HIP events per launch) -----------
+    # ---- kernel timing for the roofline: HIP events on the runner's stream bracketing one
+    # batch of back-to-back launches (the per-launch average rocprofv3's kernel trace reports)
     k_launches = min(args.steps, 2000)
     runner.set_timing(True)
     runner.rollout(k_launches)

@@ -103,8 +103,9 @@ struct cog_runner {
   uint32_t flags = 0;
   bool pending_sample = false;
   bool timing = false;
-  std::vector<hipEvent_t> ev;         // pairs
+  std::vector<hipEvent_t> ev;         // pairs: one per step() launch or one per rollout() batch
   size_t ev_used = 0;
+  uint64_t timed_launches = 0;        // fused launches covered by the recorded pairs
 };
 
 namespace {
@@ -501,25 +502,32 @@ static int runner_flush_sample(cog_runner *r) {
   return sampler_run(r->smp, masks, r->env->stream, false);
 }
 
-static int runner_launch_fused(cog_runner *r) {
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (r->timing) {
-    if (r->ev_used + 2 > r->ev.size()) {
-      for (int k = 0; k < 2; k++) {
-        hipEvent_t ev;
-        HIPCHK(hipEventCreate(&ev));
-        r->ev.push_back(ev);
-      }
-    }
-    e0 = r->ev[r->ev_used];
-    e1 = r->ev[r->ev_used + 1];
-    r->ev_used += 2;
-    HIPCHK(hipEventRecord(e0, r->env->stream));
+static int runner_timing_event(cog_runner *r, hipEvent_t *out) {
+  if (r->ev_used + 1 > r->ev.size()) {
+    hipEvent_t ev;
+    HIPCHK(hipEventCreate(&ev));
+    r->ev.push_back(ev);
   }
+  *out = r->ev[r->ev_used++];
+  HIPCHK(hipEventRecord(*out, r->env->stream));
+  return COG_OK;
+}
+
+// `steps` back-to-back fused sample+step launches; with timing on, one event pair brackets the
+// batch (device time per launch = pair time / steps, the same quantity rocprofv3's kernel
+// trace averages, without per-launch event overhead)
+static int runner_launch_fused(cog_runner *r, int steps) {
+  hipEvent_t ev;
+  int rc;
+  if (r->timing && (rc = runner_timing_event(r, &ev))) return rc;
   const int src = (r->flags & COG_RUNNER_STORED_MASKS) ? cog::MASK_STORED : cog::MASK_SELECTED;
-  if (cog::launch_sample_step(r->env->s, src, r->smp->d_rng, r->smp->d_actions, r->env->stream))
-    return fail(COG_ERR_HIP, std::string("sample_step launch failed: ") + hipGetErrorString(hipGetLastError()));
-  if (r->timing) HIPCHK(hipEventRecord(e1, r->env->stream));
+  for (int t = 0; t < steps; t++)
+    if (cog::launch_sample_step(r->env->s, src, r->smp->d_rng, r->smp->d_actions, r->env->stream))
+      return fail(COG_ERR_HIP, std::string("sample_step launch failed: ") + hipGetErrorString(hipGetLastError()));
+  if (r->timing) {
+    if ((rc = runner_timing_event(r, &ev))) return rc;
+    r->timed_launches += (uint64_t)steps;
+  }
   return COG_OK;
 }
 
@@ -537,7 +545,7 @@ int cog_runner_step(cog_runner *r) {
   DeviceGuard g(r->env->device);
   if (r->pending_sample) {
     r->pending_sample = false;
-    return runner_launch_fused(r);
+    return runner_launch_fused(r, 1);
   }
   if (cog::launch_step(r->env->s, r->smp->d_actions, r->env->stream))
     return fail(COG_ERR_HIP, std::string("step launch failed: ") + hipGetErrorString(hipGetLastError()));
@@ -549,9 +557,7 @@ int cog_runner_rollout(cog_runner *r, int steps) {
   DeviceGuard g(r->env->device);
   int rc = runner_flush_sample(r);
   if (rc) return rc;
-  for (int t = 0; t < steps; t++)
-    if ((rc = runner_launch_fused(r))) return rc;
-  return COG_OK;
+  return steps ? runner_launch_fused(r, steps) : COG_OK;
 }
 
 int cog_runner_sync(cog_runner *r) {
@@ -570,6 +576,7 @@ int cog_runner_set_timing(cog_runner *r, int enable) {
   if (!r) return fail(COG_ERR_INVALID, "runner is NULL");
   r->timing = enable != 0;
   r->ev_used = 0;
+  r->timed_launches = 0;
   return COG_OK;
 }
 
@@ -584,8 +591,9 @@ int cog_runner_kernel_time(cog_runner *r, double *total_ms, uint64_t *launches) 
     acc += ms;
   }
   if (total_ms) *total_ms = acc;
-  if (launches) *launches = r->ev_used / 2;
+  if (launches) *launches = r->timed_launches;
   r->ev_used = 0;
+  r->timed_launches = 0;
   return COG_OK;
 }
 

@@ -147,7 +147,8 @@ COG_API int cog_runner_step(cog_runner *r);      /* enqueue step(sampler actions
 COG_API int cog_runner_sync(cog_runner *r);      /* wait; refresh host views unless DEVICE_VIEWS */
 COG_API int cog_runner_rollout(cog_runner *r, int steps);   /* enqueue steps x (sample; step) */
 COG_API int cog_runner_set_timing(cog_runner *r, int enable);
-/* sum of per-launch kernel times (HIP events around each fused launch) since enabled */
+/* device time of the fused launches since enabled: HIP events bracket each step() launch and each
+   rollout() batch on the env's stream; *launches = fused launches covered */
 COG_API int cog_runner_kernel_time(cog_runner *r, double *total_ms, uint64_t *launches);
 
 #ifdef __cplusplus

@@ -8,7 +8,7 @@ import os
 import sys
 
 
-def main(d, out_json=None):
+def main(d, out_json=None, quiet=False):
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
@@ -25,6 +25,8 @@ def main(d, out_json=None):
         short = k.split("(")[0]
         res[short] = {c: sum(v) / len(v) for c, v in sorted(ctrs.items())}
         res[short]["dispatches"] = max(len(v) for v in ctrs.values())
+        if quiet:
+            continue
         print(short)
         for c, v in sorted(res[short].items()):
             print(f"   {c:28s} {v:18.1f}")
