@@ -1298,96 +1298,107 @@ DEV Plan step_env(const Ctx &e, const uint8_t act[5], Heads &sel, uint8_t *stn, 
   return o;
 }
 
+// Cooperative staging helpers.  Item it = k * 64 + lane of a record of G granules belongs to env
+// it / G, granule it % G.  Loads clamp the env to the block's last valid one (duplicate reads,
+// no branches); stores are predicated on the store plan.
+template <int G>
+DEV int item_env(int k, int lane) { return (k * 64 + lane) / G; }
+template <int G>
+DEV int item_gran(int k, int lane) { return (k * 64 + lane) % G; }
+template <int G>
+constexpr int n_items() { return (G * kWaveEnvs + 63) / 64; }
+
 // One step of the wave's 64 envs (each optionally preceded by sampling its action).
 // act_in: actions of the host API path (nullptr in the fused runner path).
+// Latency plan (one wave per SIMD at the benchmark's size, so nothing hides a stall):
+//   round 1 loads (state at fixed addresses) -> LDS -> round 2 loads (agent-dependent records)
+//   issued -> sampling on the round-1 state while they fly -> LDS -> game logic -> all LDS
+//   reads of the store phase batched -> predicated 16-B stores.
 DEV void wave_step(const DevState &s, uint32_t *slots, const uint8_t *act_in, int mask_source,
                    uint32_t *rngs, uint8_t *actions_out) {
   const int lane = threadIdx.x;
   const size_t base = (size_t)blockIdx.x * kWaveEnvs;
   const int nv = s.n - base < (size_t)kWaveEnvs ? (int)(s.n - base) : kWaveEnvs;
   auto slot_of = [&](int e) { return slots + e * kSlotWords; };
-  auto pv_of = [&](int e) { return reinterpret_cast<const EnvPriv *>(slot_of(e) + SLOT_PV / 4); };
+  auto cl = [&](int e) { return e < nv ? e : nv - 1; };
   auto obs_of = [&](int e) { return s.obs + (base + e) * COG_OBS_BYTES; };
   auto player_of = [&](int e, int p) { return obs_of(e) + COG_OBS_PLAYER0 + COG_OBS_PLAYER_STRIDE * p; };
   STAMP(s, 0);
+  const size_t i = base + (size_t)cl(lane);
+  const bool live = lane < nv;
 
-  // round 1: EnvPriv (10 granules), selected mask (6), phase/resources/shop (3)
+  // round 1: EnvPriv (10 granules), selected mask (6), phase/resources/shop (3), sampler rng
   {
-    uint4 a[kPvG], b[6], c[3];
+    constexpr int KA = n_items<kPvG>(), KB = n_items<6>(), KC = n_items<3>();
+    uint4 a[KA], b[KB], c[KC];
 #pragma unroll
-    for (int k = 0; k < kPvG; k++) {
-      const int it = k * 64 + lane, e = it / kPvG, g = it % kPvG;
-      if (e < nv) a[k] = reinterpret_cast<const uint4 *>(s.priv + base + e)[g];
-    }
+    for (int k = 0; k < KA; k++)
+      a[k] = reinterpret_cast<const uint4 *>(s.priv + base + cl(item_env<kPvG>(k, lane)))[item_gran<kPvG>(k, lane)];
 #pragma unroll
-    for (int k = 0; k < 6; k++) {
-      const int it = k * 64 + lane, e = it / 6, g = it % 6;
-      if (e < nv) b[k] = reinterpret_cast<const uint4 *>(s.sel + (base + e) * COG_MASK_BYTES)[g];
-    }
+    for (int k = 0; k < KB; k++)
+      b[k] = reinterpret_cast<const uint4 *>(s.sel + (base + cl(item_env<6>(k, lane))) * COG_MASK_BYTES)[item_gran<6>(k, lane)];
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const int it = k * 64 + lane, e = it / 3, g = it % 3;
-      if (e < nv) c[k] = reinterpret_cast<const uint4 *>(obs_of(e) + COG_OBS_PHASE)[g];
-    }
+    for (int k = 0; k < KC; k++)
+      c[k] = reinterpret_cast<const uint4 *>(obs_of(cl(item_env<3>(k, lane))) + COG_OBS_PHASE)[item_gran<3>(k, lane)];
 #pragma unroll
-    for (int k = 0; k < kPvG; k++) {
-      const int it = k * 64 + lane, e = it / kPvG, g = it % kPvG;
-      if (e < nv) lds_put4(slot_of(e) + SLOT_PV / 4 + 4 * g, a[k]);
-    }
+    for (int k = 0; k < KA; k++) lds_put4(slot_of(item_env<kPvG>(k, lane)) + SLOT_PV / 4 + 4 * item_gran<kPvG>(k, lane), a[k]);
 #pragma unroll
-    for (int k = 0; k < 6; k++) {
-      const int it = k * 64 + lane, e = it / 6, g = it % 6;
-      if (e < nv) lds_put4(slot_of(e) + SLOT_SEL / 4 + 4 * g, b[k]);
-    }
+    for (int k = 0; k < KB; k++) lds_put4(slot_of(item_env<6>(k, lane)) + SLOT_SEL / 4 + 4 * item_gran<6>(k, lane), b[k]);
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const int it = k * 64 + lane, e = it / 3, g = it % 3;
-      if (e < nv) lds_put4(slot_of(e) + SLOT_SH / 4 + 4 * g, c[k]);
-    }
+    for (int k = 0; k < KC; k++) lds_put4(slot_of(item_env<3>(k, lane)) + SLOT_SH / 4 + 4 * item_gran<3>(k, lane), c[k]);
   }
+  uint32_t rng = act_in ? 0u : rngs[i];
   __syncthreads();
 
-  // round 2 (addresses depend on the agent): deck + stored mask of a0 (13 granules, skipping
-  // the DeckObs padding granule), stored mask of na (6)
-  {
-    uint4 a[13], b[6];
+  // round 2 (addresses depend on the agent): deck + stored mask of a0 (13 granules, skipping the
+  // DeckObs padding granule), stored mask of na (6).  Issued, then the sampler runs on the
+  // round-1 state while they are in flight.
+  uint32_t *slot = slot_of(lane);
+  uint8_t *lds = reinterpret_cast<uint8_t *>(slot);
+  EnvPriv *pv = reinterpret_cast<EnvPriv *>(lds + SLOT_PV);
+  const int a0 = pv->agent;
+  const int na = a0 + 1 >= pv->n_players ? 0 : a0 + 1;
+  const int players = a0 | na << 2;                        // this lane's env: a0, na
+  constexpr int KD = n_items<13>(), KE = n_items<6>();
+  uint4 dk[KD], sn[KE];
 #pragma unroll
-    for (int k = 0; k < 13; k++) {
-      const int it = k * 64 + lane, e = it / 13, g = it % 13;
-      if (e < nv) a[k] = reinterpret_cast<const uint4 *>(player_of(e, pv_of(e)->agent))[g < 7 ? g : g + 1];
-    }
+  for (int k = 0; k < KD; k++) {
+    const int e = item_env<13>(k, lane), g = item_gran<13>(k, lane);
+    const int pa = __shfl(players, cl(e)) & 3;
+    dk[k] = reinterpret_cast<const uint4 *>(player_of(cl(e), pa))[g < 7 ? g : g + 1];
+  }
 #pragma unroll
-    for (int k = 0; k < 6; k++) {
-      const int it = k * 64 + lane, e = it / 6, g = it % 6;
-      if (e < nv) {
-        const EnvPriv *pv = pv_of(e);
-        const int na = pv->agent + 1 >= pv->n_players ? 0 : pv->agent + 1;
-        b[k] = reinterpret_cast<const uint4 *>(player_of(e, na) + COG_PD_MASK)[g];
+  for (int k = 0; k < KE; k++) {
+    const int e = item_env<6>(k, lane), g = item_gran<6>(k, lane);
+    const int pn = __shfl(players, cl(e)) >> 2;
+    sn[k] = reinterpret_cast<const uint4 *>(player_of(cl(e), pn) + COG_PD_MASK)[g];
+  }
+  Heads sel = heads_from(lds + SLOT_SEL);
+  uint8_t act[5] = {0, 0, 0, 0, 0};
+  if (act_in) {                                            // host actions: indices past a head
+    const uint8_t *ai = act_in + i * COG_ACTION_BYTES;     // are the reference's OOB accesses
+    const uint8_t top[5] = {COG_N_CARDTYPES, COG_N_CARDTYPES, COG_N_CARDTYPES, 6, COG_N_SHOP};
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+      act[k] = ai[k];
+      if (act[k] > top[k]) {
+        act[k] = top[k];
+        if (live) pv->flags |= F_BAD_ACTION;
       }
     }
-#pragma unroll
-    for (int k = 0; k < 13; k++) {
-      const int it = k * 64 + lane, e = it / 13, g = it % 13;
-      if (e < nv) lds_put4(slot_of(e) + SLOT_DK / 4 + 4 * g, a[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < 6; k++) {
-      const int it = k * 64 + lane, e = it / 6, g = it % 6;
-      if (e < nv) lds_put4(slot_of(e) + SLOT_STN / 4 + 4 * g, b[k]);
-    }
+  } else if (mask_source != MASK_STORED) {                 // runner: sample(selected masks)
+    sample_heads(sel, rng, act);
   }
+#pragma unroll
+  for (int k = 0; k < KD; k++) lds_put4(slot_of(item_env<13>(k, lane)) + SLOT_DK / 4 + 4 * item_gran<13>(k, lane), dk[k]);
+#pragma unroll
+  for (int k = 0; k < KE; k++) lds_put4(slot_of(item_env<6>(k, lane)) + SLOT_STN / 4 + 4 * item_gran<6>(k, lane), sn[k]);
   __syncthreads();
   STAMP(s, 1);
 
   // per-lane game logic on the slot of env `lane`
-  const size_t i = base + lane;
   bool enc = false;
-  if (lane < nv) {
-    uint32_t *slot = slot_of(lane);
-    uint8_t *lds = reinterpret_cast<uint8_t *>(slot);
-    EnvPriv *pv = reinterpret_cast<EnvPriv *>(lds + SLOT_PV);
-    const int a0 = pv->agent;
-    const int na = a0 + 1 >= pv->n_players ? 0 : a0 + 1;
+  if (live) {
     Ctx e;
     e.ob = s.obs + i * COG_OBS_BYTES;
     e.sh = lds + SLOT_SH;
@@ -1403,22 +1414,8 @@ DEV void wave_step(const DevState &s, uint32_t *slots, const uint8_t *act_in, in
     e.gs = s.gen + i;
     e.stamps = s.stamps;
 
-    Heads sel = heads_from(e.sel);
-    uint8_t act[5];
-    if (act_in) {                                          // host actions: indices past a head
-      const uint8_t *ai = act_in + i * COG_ACTION_BYTES;   // are the reference's OOB accesses
-      const uint8_t top[5] = {COG_N_CARDTYPES, COG_N_CARDTYPES, COG_N_CARDTYPES, 6, COG_N_SHOP};
-      for (int k = 0; k < 5; k++) {
-        act[k] = ai[k];
-        if (act[k] > top[k]) {
-          act[k] = top[k];
-          pv->flags |= F_BAD_ACTION;
-        }
-      }
-    } else {                                               // runner: sample(selected | stored mask)
-      uint32_t rng = rngs[i];
-      if (mask_source == MASK_STORED) sample_heads(heads_from(e.sta), rng, act);
-      else sample_heads(sel, rng, act);
+    if (!act_in) {
+      if (mask_source == MASK_STORED) sample_heads(heads_from(e.sta), rng, act);   // runner, stored masks
       rngs[i] = rng;
       store_action(actions_out + i * COG_ACTION_BYTES, act);
     }
@@ -1446,47 +1443,75 @@ DEV void wave_step(const DevState &s, uint32_t *slots, const uint8_t *act_in, in
     slot[SLOT_PLAN / 4] = o.pv | o.sh << 10 | o.dk << 13 | o.st << 20 | o.stn << 26;
     slot[SLOT_PLAN / 4 + 1] = (uint32_t)a0 | (uint32_t)na << 2;   // records of the ORIGINAL agent
     STAMP(s, 11);
+  } else {
+    slot[SLOT_PLAN / 4] = 0u;                              // lanes past the batch store nothing
   }
   __syncthreads();
 
-  // cooperative stores of the dirty granules
+  // cooperative stores of the dirty granules: every LDS read first (one wait), then the stores
+  {
+    constexpr int KA = n_items<kPvG>(), KB = n_items<6>(), KC = n_items<3>();
+    uint4 va[KA], vb[KB], vc[KC], vd[KD], ve[KE];
+    uint32_t pa[KA], pc[KC], pd[KD], pe[KE], wd[KD], we[KE];
 #pragma unroll
-  for (int k = 0; k < kPvG; k++) {
-    const int it = k * 64 + lane, e = it / kPvG, g = it % kPvG;
-    if (e < nv && ((slot_of(e)[SLOT_PLAN / 4] >> g) & 1u))
-      reinterpret_cast<uint4 *>(s.priv + base + e)[g] = lds_get4(slot_of(e) + SLOT_PV / 4 + 4 * g);
-  }
-#pragma unroll
-  for (int k = 0; k < 6; k++) {
-    const int it = k * 64 + lane, e = it / 6, g = it % 6;
-    if (e < nv) reinterpret_cast<uint4 *>(s.sel + (base + e) * COG_MASK_BYTES)[g] = lds_get4(slot_of(e) + SLOT_SEL / 4 + 4 * g);
-  }
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    const int it = k * 64 + lane, e = it / 3, g = it % 3;
-    if (e < nv && ((slot_of(e)[SLOT_PLAN / 4] >> (10 + g)) & 1u))
-      reinterpret_cast<uint4 *>(obs_of(e) + COG_OBS_PHASE)[g] = lds_get4(slot_of(e) + SLOT_SH / 4 + 4 * g);
-  }
-#pragma unroll
-  for (int k = 0; k < 13; k++) {                           // deck granules = plan bits 13..19,
-    const int it = k * 64 + lane, e = it / 13, g = it % 13; // stored-mask granules = bits 20..25
-    const uint32_t plan = e < nv ? slot_of(e)[SLOT_PLAN / 4] : 0u;
-    if ((plan >> (13 + g)) & 1u) {
-      uint8_t *p = player_of(e, slot_of(e)[SLOT_PLAN / 4 + 1] & 3u);
-      reinterpret_cast<uint4 *>(p)[g < 7 ? g : g + 1] = lds_get4(slot_of(e) + SLOT_DK / 4 + 4 * g);
+    for (int k = 0; k < KA; k++) {
+      const int e = item_env<kPvG>(k, lane), g = item_gran<kPvG>(k, lane);
+      pa[k] = (slot_of(e)[SLOT_PLAN / 4] >> g) & 1u;
+      va[k] = lds_get4(slot_of(e) + SLOT_PV / 4 + 4 * g);
     }
-  }
 #pragma unroll
-  for (int k = 0; k < 6; k++) {                            // na's stored mask = bits 26..31
-    const int it = k * 64 + lane, e = it / 6, g = it % 6;
-    const uint32_t plan = e < nv ? slot_of(e)[SLOT_PLAN / 4] : 0u;
-    if ((plan >> (26 + g)) & 1u) {
-      uint8_t *p = player_of(e, (slot_of(e)[SLOT_PLAN / 4 + 1] >> 2) & 3u) + COG_PD_MASK;
-      reinterpret_cast<uint4 *>(p)[g] = lds_get4(slot_of(e) + SLOT_STN / 4 + 4 * g);
+    for (int k = 0; k < KB; k++) {
+      const int e = item_env<6>(k, lane), g = item_gran<6>(k, lane);
+      vb[k] = lds_get4(slot_of(e) + SLOT_SEL / 4 + 4 * g);
+    }
+#pragma unroll
+    for (int k = 0; k < KC; k++) {
+      const int e = item_env<3>(k, lane), g = item_gran<3>(k, lane);
+      pc[k] = (slot_of(e)[SLOT_PLAN / 4] >> (10 + g)) & 1u;
+      vc[k] = lds_get4(slot_of(e) + SLOT_SH / 4 + 4 * g);
+    }
+#pragma unroll
+    for (int k = 0; k < KD; k++) {                         // deck granules = plan bits 13..19,
+      const int e = item_env<13>(k, lane), g = item_gran<13>(k, lane);   // stored mask = bits 20..25
+      pd[k] = (slot_of(e)[SLOT_PLAN / 4] >> (13 + g)) & 1u;
+      wd[k] = slot_of(e)[SLOT_PLAN / 4 + 1] & 3u;
+      vd[k] = lds_get4(slot_of(e) + SLOT_DK / 4 + 4 * g);
+    }
+#pragma unroll
+    for (int k = 0; k < KE; k++) {                         // na's stored mask = bits 26..31
+      const int e = item_env<6>(k, lane), g = item_gran<6>(k, lane);
+      pe[k] = (slot_of(e)[SLOT_PLAN / 4] >> (26 + g)) & 1u;
+      we[k] = (slot_of(e)[SLOT_PLAN / 4 + 1] >> 2) & 3u;
+      ve[k] = lds_get4(slot_of(e) + SLOT_STN / 4 + 4 * g);
+    }
+#pragma unroll
+    for (int k = 0; k < KA; k++) {
+      const int e = item_env<kPvG>(k, lane), g = item_gran<kPvG>(k, lane);
+      if (pa[k]) reinterpret_cast<uint4 *>(s.priv + base + e)[g] = va[k];
+    }
+#pragma unroll
+    for (int k = 0; k < KB; k++) {
+      const int e = item_env<6>(k, lane), g = item_gran<6>(k, lane);
+      if (e < nv) reinterpret_cast<uint4 *>(s.sel + (base + e) * COG_MASK_BYTES)[g] = vb[k];
+    }
+#pragma unroll
+    for (int k = 0; k < KC; k++) {
+      const int e = item_env<3>(k, lane), g = item_gran<3>(k, lane);
+      if (pc[k]) reinterpret_cast<uint4 *>(obs_of(e) + COG_OBS_PHASE)[g] = vc[k];
+    }
+#pragma unroll
+    for (int k = 0; k < KD; k++) {
+      const int e = item_env<13>(k, lane), g = item_gran<13>(k, lane);
+      if (pd[k]) reinterpret_cast<uint4 *>(player_of(e, wd[k]))[g < 7 ? g : g + 1] = vd[k];
+    }
+#pragma unroll
+    for (int k = 0; k < KE; k++) {
+      const int e = item_env<6>(k, lane), g = item_gran<6>(k, lane);
+      if (pe[k]) reinterpret_cast<uint4 *>(player_of(e, we[k]) + COG_PD_MASK)[g] = ve[k];
     }
   }
   STAMP(s, 12);
-  wave_encode(s, i, enc);
+  wave_encode(s, base + lane, enc);
 }
 
 __global__ void __launch_bounds__(64) k_step(DevState s, const uint8_t *__restrict__ actions) {
