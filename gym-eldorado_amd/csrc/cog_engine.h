@@ -92,6 +92,7 @@ struct DevState {
   EnvPriv *priv;
   uint8_t *grid;
   uint8_t *cgrid;                    // [n] x 2304 B compact 48x48 hex codes (lookups + encode)
+  uint4 *heads;                      // [n][5] mask bit-vectors: selected, stored of players 0..3
   GenScratch *gen;
   uint32_t *status;                  // [0] OR of error flags, [1] error count, [2] dirty count
   uint32_t *dirty;                   // [n] envs whose map was re-generated (host view refresh)

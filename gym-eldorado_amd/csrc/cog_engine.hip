@@ -16,8 +16,10 @@
 //   k_reset          cog_env::reset(params) incl. procedural map generation (map.cpp:697-742)
 //   k_encode         48x48x7 map-observation encode (map.cpp:389-405): streaming, 16 cells / item
 //   k_sample         masked uniform sampler (sampler.h:14-79)
-//   k_step           vec_cog_env::step with auto-reset (vec_environment.h:46-61)
-//   k_sample_step    runner-fused sample(selected|stored masks) + step (runner.h:46-55)
+//   k_env_step<SRC>  vec_cog_env::step with auto-reset (vec_environment.h:46-61); SRC: host
+//                    actions, or the runner-fused sample(selected | stored masks) + step
+//                    (runner.h:46-55)
+//   k_sync_heads     mask bit-vectors of every env from its byte records (init / reset)
 #include <hip/hip_runtime.h>
 
 #include "cog_engine.h"
@@ -677,58 +679,6 @@ DEV void wave_encode(const DevState &s, size_t i, bool enc) {
 }
 
 // ------------------------------------------------------------------------------------------
-// sampler (sampler.h:14-79): 5 independent uniform picks over the set bits of each head
-// ------------------------------------------------------------------------------------------
-DEV uint32_t bools4(uint32_t w) {                          // 4 bool bytes -> 4 bits (nonzero = set)
-  const uint32_t nz = (((w & 0x7f7f7f7fu) + 0x7f7f7f7fu) | w) & 0x80808080u;
-  return ((nz >> 7) * 0x01020408u) >> 24 & 0xfu;
-}
-DEV uint32_t nth_set_bit(uint32_t m, uint32_t j) {        // index of the j-th (0-based) set bit
-  uint32_t base = 0;
-  uint32_t c = __popc(m & 0xffffu);
-  if (j >= c) { j -= c; base += 16; m >>= 16; }
-  c = __popc(m & 0xffu);
-  if (j >= c) { j -= c; base += 8; m >>= 8; }
-  c = __popc(m & 0xfu);
-  if (j >= c) { j -= c; base += 4; m >>= 4; }
-  c = __popc(m & 0x3u);
-  if (j >= c) { j -= c; base += 2; m >>= 2; }
-  c = m & 1u;
-  if (j >= c) { base += 1; }
-  return base;
-}
-DEV uint8_t pick(uint32_t &rng, uint32_t m) {
-  const uint32_t k = __popc(m);
-  if (!k) return 0;
-  return (uint8_t)nth_set_bit(m, uid(rng, k));
-}
-DEV void sample_mask(const uint8_t *mask, uint32_t &rng, uint8_t out[5]) {
-  const uint32_t *m32 = reinterpret_cast<const uint32_t *>(mask);   // 4-byte aligned (LDS slot or record)
-  uint64_t lo = 0, hi = 0;
-#pragma unroll
-  for (int word = 0; word < 23; word++) {                  // bytes 4*word .. 4*word+3
-    const uint64_t b = bools4(m32[word]);
-    const int bit = 4 * word;
-    if (bit < 64) lo |= b << bit;
-    else hi |= b << (bit - 64);
-  }
-  const uint32_t play = (uint32_t)(lo & 0x3fffffu);
-  const uint32_t spec = (uint32_t)((lo >> 22) & 0x3fffffu);
-  const uint32_t rem = (uint32_t)(((lo >> 44) | (hi << 20)) & 0x3fffffu);
-  const uint32_t mov = (uint32_t)((hi >> 2) & 0x7fu);
-  const uint32_t shop = (uint32_t)((hi >> 9) & 0x7ffffu);
-  out[0] = pick(rng, play);
-  out[1] = pick(rng, spec);
-  out[2] = pick(rng, rem);
-  out[3] = pick(rng, mov);
-  out[4] = pick(rng, shop);
-}
-DEV void store_action(uint8_t *dst, const uint8_t a[5]) {
-  const uint32_t lo = (uint32_t)a[0] | (uint32_t)a[1] << 8 | (uint32_t)a[2] << 16 | (uint32_t)a[3] << 24;
-  reinterpret_cast<uint2 *>(dst)[0] = make_uint2(lo, (uint32_t)a[4]);
-}
-
-// ------------------------------------------------------------------------------------------
 // kernels
 // ------------------------------------------------------------------------------------------
 __global__ void k_init(DevState s, uint32_t default_seed) {
@@ -830,552 +780,634 @@ __global__ void __launch_bounds__(256) k_encode_lds(const uint8_t *__restrict__ 
   }
 }
 
-// ---- per-env LDS slots of a step's working set, staged by the whole wave ------------------
-// slot = 155 dwords (odd stride: same-offset dword accesses of a wave are bank-conflict free)
-//   [  0,160) EnvPriv                 [160,256) selected ActionMask (96 B)
-//   [256,304) ObsData 16128..16175 (phase, resources, shop)
-//   [304,416) DeckObs of the acting player a0 (112 B)   [416,512) stored ActionMask of a0
-//   [512,608) stored ActionMask of the next player na (the turn change reads it)
-//   [608,616) store plan: dirty 16-B granules of each staged record
-// Loads and stores are cooperative: item (env e, granule g) of a record goes to lane
-// (e * G + g) mod 64, so one instruction covers 64 / G whole records instead of 64 scattered
-// 16-B pieces; the game logic then runs one env per lane on its slot.
-constexpr int kSlotWords = 155;
-constexpr int SLOT_PV = 0, SLOT_SEL = 160, SLOT_SH = 256, SLOT_DK = 304, SLOT_ST = 416, SLOT_STN = 512,
-              SLOT_PLAN = 608;
-constexpr int kPvG = (int)sizeof(EnvPriv) / 16;          // 10 granules
-constexpr int kWaveEnvs = 64;
-
-DEV void lds_put4(uint32_t *d, const uint4 &v) { d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w; }
-DEV uint4 lds_get4(const uint32_t *d) { return make_uint4(d[0], d[1], d[2], d[3]); }
-
-// ---- fast path: play / pass / turn change on registers (environment.cpp:91-250) -------------
-// Selected and stored masks are held as five head bitsets (bit k == index k of the head); the
-// deck's bulk operations run on dwords with compile-time byte positions.  Move / shop / remove /
-// special actions and resets take the byte-level path above (env_step / env_reset).
-struct Heads {
+// ------------------------------------------------------------------------------------------
+// Mask bit-vectors.  The step keeps every ActionMask as its 92 named bytes packed into bits
+// (bit k == byte k != 0): w0 = bytes 0..31, w1 = 32..63, w2 = 64..91.  One 16-B record per mask
+// in DevState::heads: [5 i] the selected mask, [5 i + 1 + p] the stored mask of player p.  The
+// byte records (ObsData / selected_action_masks) are the outputs; the step never reads them.
+// ------------------------------------------------------------------------------------------
+struct Heads {                        // the five heads of one mask (sampler.h:14-79)
   uint32_t play, spec, rem, move, shop;
 };
+struct MBits {
+  uint32_t w0, w1, w2;
+};
 
-DEV Heads heads_from(const uint8_t *mask) {               // ActionMask bytes -> bitsets
-  const uint32_t *m32 = reinterpret_cast<const uint32_t *>(mask);
-  uint64_t lo = 0, hi = 0;
-#pragma unroll
-  for (int w = 0; w < 23; w++) {
-    const uint64_t b = bools4(m32[w]);
-    if (4 * w < 64) lo |= b << (4 * w);
-    else hi |= b << (4 * w - 64);
-  }
+DEV Heads heads_of(const MBits &b) {
   Heads h;
-  h.play = (uint32_t)(lo & 0x3fffffu);
-  h.spec = (uint32_t)((lo >> 22) & 0x3fffffu);
-  h.rem = (uint32_t)(((lo >> 44) | (hi << 20)) & 0x3fffffu);
-  h.move = (uint32_t)((hi >> 2) & 0x7fu);
-  h.shop = (uint32_t)((hi >> 9) & 0x7ffffu);
+  h.play = b.w0 & 0x3fffffu;
+  h.spec = ((b.w0 >> 22) | (b.w1 << 10)) & 0x3fffffu;
+  h.rem = ((b.w1 >> 12) | (b.w2 << 20)) & 0x3fffffu;
+  h.move = (b.w2 >> 2) & 0x7fu;
+  h.shop = (b.w2 >> 9) & 0x7ffffu;
   return h;
 }
-DEV uint32_t expand4(uint32_t x) { return (x * 0x00204081u) & 0x01010101u; }   // 4 bits -> 4 bool bytes
-DEV void heads_to(const Heads &h, uint32_t *m32) {        // bitsets -> the 23 named dwords
-  const uint64_t lo = (uint64_t)h.play | ((uint64_t)h.spec << 22) | ((uint64_t)h.rem << 44);
-  const uint64_t hi = ((uint64_t)h.rem >> 20) | ((uint64_t)h.move << 2) | ((uint64_t)h.shop << 9);
-#pragma unroll
-  for (int w = 0; w < 23; w++)
-    m32[w] = expand4((uint32_t)((4 * w < 64 ? lo >> (4 * w) : hi >> (4 * w - 64)) & 0xfu));
+DEV MBits bits_of(const Heads &h) {
+  MBits b;
+  b.w0 = h.play | (h.spec << 22);
+  b.w1 = (h.spec >> 10) | (h.rem << 12);
+  b.w2 = (h.rem >> 20) | (h.move << 2) | (h.shop << 9);
+  return b;
 }
-DEV void sample_heads(const Heads &h, uint32_t &rng, uint8_t out[5]) {      // sampler.h:14-79
+DEV MBits mbits_of(const uint4 &v) { return MBits{v.x, v.y, v.z}; }
+DEV uint4 mbits_u4(const MBits &b) { return make_uint4(b.w0, b.w1, b.w2, 0u); }
+
+DEV uint32_t bools4(uint32_t w) {                          // 4 bool bytes -> 4 bits (nonzero = set)
+  const uint32_t nz = (((w & 0x7f7f7f7fu) + 0x7f7f7f7fu) | w) & 0x80808080u;
+  return ((nz >> 7) * 0x01020408u) >> 24 & 0xfu;
+}
+DEV uint32_t expand4(uint32_t x) { return (x * 0x00204081u) & 0x01010101u; }   // 4 bits -> 4 bool bytes
+
+DEV MBits mbits_from_bytes(const uint8_t *mask) {          // ActionMask bytes -> bits (4-B aligned)
+  const uint32_t *m32 = reinterpret_cast<const uint32_t *>(mask);
+  MBits b{0u, 0u, 0u};
+#pragma unroll
+  for (int w = 0; w < 23; w++) {
+    const uint32_t v = bools4(m32[w]) << (4 * (w & 7));
+    if (w < 8) b.w0 |= v;
+    else if (w < 16) b.w1 |= v;
+    else b.w2 |= v;
+  }
+  return b;
+}
+DEV uint32_t mask_dword(const MBits &b, int q) {           // named dword q (bytes 4q..4q+3), q < 24
+  const uint32_t w = q < 8 ? b.w0 : (q < 16 ? b.w1 : b.w2);
+  return q < 23 ? expand4((w >> (4 * (q & 7))) & 0xfu) : 0u;
+}
+DEV uint4 mask_granule(const MBits &b, int g) {            // 16-B granule g (0..5) of the record
+  return make_uint4(mask_dword(b, 4 * g), mask_dword(b, 4 * g + 1), mask_dword(b, 4 * g + 2), mask_dword(b, 4 * g + 3));
+}
+DEV uint32_t mask_diff_granules(const MBits &a, const MBits &b) {   // granules whose bytes differ
+  const uint32_t x0 = a.w0 ^ b.w0, x1 = a.w1 ^ b.w1, x2 = a.w2 ^ b.w2;
+  return ((x0 & 0xffffu) ? 1u : 0u) | ((x0 >> 16) ? 2u : 0u) | ((x1 & 0xffffu) ? 4u : 0u) | ((x1 >> 16) ? 8u : 0u) |
+         ((x2 & 0xffffu) ? 16u : 0u) | ((x2 >> 16) ? 32u : 0u);
+}
+
+// heads of every mask of env i from its byte records (after init / reset / auto-reset)
+DEV void sync_heads(const DevState &s, size_t i) {
+  uint4 *h = s.heads + 5 * i;
+  h[0] = mbits_u4(mbits_from_bytes(s.sel + i * COG_MASK_BYTES));
+  const uint8_t *ob = s.obs + i * COG_OBS_BYTES + COG_OBS_PLAYER0 + COG_PD_MASK;
+#pragma unroll
+  for (int p = 0; p < 4; p++) h[1 + p] = mbits_u4(mbits_from_bytes(ob + COG_OBS_PLAYER_STRIDE * p));
+}
+
+// ------------------------------------------------------------------------------------------
+// sampler (sampler.h:14-79): 5 independent uniform picks over the set bits of each head
+// ------------------------------------------------------------------------------------------
+DEV uint32_t nth_set_bit(uint32_t m, uint32_t j) {        // index of the j-th (0-based) set bit
+  uint32_t base = 0;
+  uint32_t c = __popc(m & 0xffffu);
+  if (j >= c) { j -= c; base += 16; m >>= 16; }
+  c = __popc(m & 0xffu);
+  if (j >= c) { j -= c; base += 8; m >>= 8; }
+  c = __popc(m & 0xfu);
+  if (j >= c) { j -= c; base += 4; m >>= 4; }
+  c = __popc(m & 0x3u);
+  if (j >= c) { j -= c; base += 2; m >>= 2; }
+  c = m & 1u;
+  if (j >= c) { base += 1; }
+  return base;
+}
+DEV uint8_t pick(uint32_t &rng, uint32_t m) {
+  const uint32_t k = __popc(m);
+  if (!k) return 0;
+  return (uint8_t)nth_set_bit(m, uid(rng, k));
+}
+DEV void sample_heads(const Heads &h, uint32_t &rng, uint8_t out[5]) {
   out[0] = pick(rng, h.play);
   out[1] = pick(rng, h.spec);
   out[2] = pick(rng, h.rem);
   out[3] = pick(rng, h.move);
   out[4] = pick(rng, h.shop);
 }
-DEV uint32_t set_bit(uint32_t m, int k, bool v) { return v ? (m | (1u << k)) : (m & ~(1u << k)); }
+DEV void sample_mask(const uint8_t *mask, uint32_t &rng, uint8_t out[5]) {
+  sample_heads(heads_of(mbits_from_bytes(mask)), rng, out);
+}
+DEV void store_action(uint8_t *dst, const uint8_t a[5]) {
+  const uint32_t lo = (uint32_t)a[0] | (uint32_t)a[1] << 8 | (uint32_t)a[2] << 16 | (uint32_t)a[3] << 24;
+  reinterpret_cast<uint2 *>(dst)[0] = make_uint2(lo, (uint32_t)a[4]);
+}
 
+// ------------------------------------------------------------------------------------------
+// Register-resident step (cog_env::step, environment.cpp:91-288).  Each work-item loads its
+// env's working set (~300 B) straight into VGPRs in two rounds (fixed-address records, then the
+// acting player's records), runs the game logic on registers only, and stores back the 16-B
+// granules that changed.  Card / shop tables are compile-time bit-packed constants, so no
+// divergent table loads sit on the critical path.
+// ------------------------------------------------------------------------------------------
 constexpr cog_card_t kCards[COG_N_CARDTYPES] = COG_CARD_TABLE;
 constexpr uint8_t kShopTypes[COG_N_SHOP] = COG_SHOP_TYPES;
 constexpr uint32_t kSpecialBits = 0x1f8000u;              // card types 15..20
 
-DEV uint32_t byte_of(const uint32_t *w, int idx) { return (w[idx >> 2] >> (8 * (idx & 3))) & 0xffu; }
-DEV void put_byte(uint32_t *w, int idx, uint32_t v) {
-  const int sh = 8 * (idx & 3);
-  w[idx >> 2] = (w[idx >> 2] & ~(0xffu << sh)) | ((v & 0xffu) << sh);
+enum CardField { CF_RES0, CF_RES1, CF_RES2, CF_COST, CF_SPECIAL, CF_SINGLE };
+constexpr uint32_t card_field(int c, int f) {
+  return f == CF_COST ? kCards[c].cost : f == CF_SPECIAL ? kCards[c].special : f == CF_SINGLE ? kCards[c].single_use
+                                                                                             : kCards[c].res[f];
 }
+constexpr uint64_t pack3(int f) {                          // 21 cards x 3 bits
+  uint64_t v = 0;
+  for (int c = 0; c < COG_N_CARDTYPES; c++) v |= (uint64_t)(card_field(c, f) & 7u) << (3 * c);
+  return v;
+}
+constexpr uint64_t kRes0 = pack3(CF_RES0), kRes1 = pack3(CF_RES1), kRes2 = pack3(CF_RES2);
+constexpr uint64_t kCost = pack3(CF_COST), kSpecial = pack3(CF_SPECIAL), kSingle = pack3(CF_SINGLE);
+constexpr uint32_t shop_cost_mask(int v) {                 // shop slots whose card costs v
+  uint32_t m = 0;
+  for (int i = 0; i < COG_N_SHOP; i++) m |= (kCards[kShopTypes[i]].cost == v ? 1u : 0u) << i;
+  return m;
+}
+static_assert(pack3(CF_RES0) >> 63 == 0, "3-bit card fields");
 
-// Deck::discard_all_active + discard_all_played (cards.cpp:219-232) on dwords 10..26
-DEV void fast_discard_all(uint32_t *dk32) {
-  uint32_t w[17];
+constexpr uint32_t kCostMask1 = shop_cost_mask(1), kCostMask2 = shop_cost_mask(2), kCostMask3 = shop_cost_mask(3),
+                   kCostMask4 = shop_cost_mask(4), kCostMask5 = shop_cost_mask(5);
+constexpr int shop_type(int k) { return k < 4 ? k + 1 : (k == 4 ? 6 : k + 3); }   // COG_SHOP_TYPES
+constexpr bool shop_types_ok() {
+  for (int k = 0; k < COG_N_SHOP; k++)
+    if (shop_type(k) != kShopTypes[k]) return false;
+  return (kCostMask1 | kCostMask2 | kCostMask3 | kCostMask4 | kCostMask5) == 0x3ffffu;
+}
+static_assert(shop_types_ok(), "shop slot -> card type formula / cost masks");
+
+DEV uint32_t cardf(uint64_t table, int c) { return (uint32_t)(table >> (3 * c)) & 7u; }
+DEV uint32_t set_bit(uint32_t m, int k, bool v) { return v ? (m | (1u << k)) : (m & ~(1u << k)); }
+
+// DeckObs bytes 0..111 in 28 dwords: constant-position accessors, and dynamic-index accessors
+// that select over the dwords a 21-byte pile can touch (u8 wrap-around, like the reference)
+DEV uint32_t dk_get(const uint32_t *d, int b) { return (d[b >> 2] >> (8 * (b & 3))) & 0xffu; }
+DEV void dk_put(uint32_t *d, int b, uint32_t v) {
+  const int sh = 8 * (b & 3);
+  d[b >> 2] = (d[b >> 2] & ~(0xffu << sh)) | ((v & 0xffu) << sh);
+}
+template <int LO, int HI>                                  // byte index in [LO, HI]
+DEV uint32_t dk_getv(const uint32_t *d, int b) {
+  const int q = b >> 2;
+  uint32_t w = 0;
 #pragma unroll
-  for (int q = 0; q < 17; q++) w[q] = dk32[10 + q];
+  for (int k = LO >> 2; k <= (HI >> 2); k++) w = k == q ? d[k] : w;
+  return (w >> (8 * (b & 3))) & 0xffu;
+}
+template <int LO, int HI>
+DEV void dk_addv(uint32_t *d, int b, uint32_t delta) {
+  const int q = b >> 2;
+  const uint32_t sh = 8 * (b & 3), m = 0xffu << sh;
+#pragma unroll
+  for (int k = LO >> 2; k <= (HI >> 2); k++) {
+    const uint32_t t = ((d[k] + (delta << sh)) & m) | (d[k] & ~m);
+    d[k] = k == q ? t : d[k];
+  }
+}
+template <int BASE>
+DEV uint32_t pile_get(const uint32_t *d, int c) { return dk_getv<BASE, BASE + 20>(d, BASE + c); }
+template <int BASE>
+DEV void pile_add(uint32_t *d, int c, uint32_t delta) { dk_addv<BASE, BASE + 20>(d, BASE + c, delta); }
+
+// c = number of k in [0, 21) whose prefix sum pile[0] + .. + pile[k] <= t: the index the
+// reference's draw-pile scan stops at (cards.cpp:196-201) while the pile holds more than t
+template <int BASE>
+DEV uint32_t pile_scan(const uint32_t *d, uint32_t t) {
+  uint32_t s = 0, c = 0;
 #pragma unroll
   for (int k = 0; k < COG_N_CARDTYPES; k++) {
-    const uint32_t a = byte_of(w, COG_DECK_ACTIVE + k - 40), p = byte_of(w, COG_DECK_PLAYED + k - 40);
-    put_byte(w, COG_DECK_DISCARD + k - 40, byte_of(w, COG_DECK_DISCARD + k - 40) + a + p);
-    put_byte(w, COG_DECK_ACTIVE + k - 40, 0u);
-    put_byte(w, COG_DECK_PLAYED + k - 40, 0u);
+    s += dk_get(d, BASE + k);
+    c += s <= t ? 1u : 0u;
   }
-#pragma unroll
-  for (int q = 0; q < 17; q++) dk32[10 + q] = w[q];
+  return c;
 }
 
-// Deck::move_discard_to_draw (cards.cpp:234-240): draw dwords 0..5, discard dwords 21..26
-DEV void fast_move_discard_to_draw(uint32_t *dk32, PlayerPriv &P) {
-  uint32_t d[6], x[6];
+struct PState {                       // PlayerPriv unpacked (player.h:60-75, cards.h:137-145)
+  uint32_t has_won, mip, n_removes, next_card_free, next_move_free, n_in_hand, n_active, n_in_draw;
+  uint32_t idx_last, steps_taken, n_added_cards, pad, n_movements;
+};
+DEV PState unpack_player(const uint4 &v) {
+  PState P;
+  P.has_won = v.x & 0xffu; P.mip = (v.x >> 8) & 0xffu; P.n_removes = (v.x >> 16) & 0xffu; P.next_card_free = v.x >> 24;
+  P.next_move_free = v.y & 0xffu; P.n_in_hand = (v.y >> 8) & 0xffu; P.n_active = (v.y >> 16) & 0xffu; P.n_in_draw = v.y >> 24;
+  P.idx_last = v.z & 0xffu; P.steps_taken = (v.z >> 8) & 0xffu; P.n_added_cards = (v.z >> 16) & 0xffu; P.pad = v.z >> 24;
+  P.n_movements = v.w;
+  return P;
+}
+DEV uint32_t b4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return (a & 0xffu) | (b & 0xffu) << 8 | (c & 0xffu) << 16 | (d & 0xffu) << 24;
+}
+DEV uint4 pack_player(const PState &P) {
+  return make_uint4(b4(P.has_won, P.mip, P.n_removes, P.next_card_free),
+                    b4(P.next_move_free, P.n_in_hand, P.n_active, P.n_in_draw),
+                    b4(P.idx_last, P.steps_taken, P.n_added_cards, P.pad), P.n_movements);
+}
+DEV bool ne4(const uint4 &a, const uint4 &b) { return ((a.x ^ b.x) | (a.y ^ b.y) | (a.z ^ b.z) | (a.w ^ b.w)) != 0u; }
+
+struct RegEnv {
+  // EnvPriv granules 0/1 (unpacked fields) and the Info mirror (granule 3, dword 0)
+  uint32_t rng, seed, max_steps, turn_counter;
+  uint32_t g1x, g1y, in_market, flags;                    // g1x: n_players n_pieces difficulty done
+  uint32_t info_steps;
+  PState P;                                                // acting player ag
+  uint32_t na_active;                                      // n_active of the next player na
+  uint2 cells_a, cells_n;                                  // neighbourhood caches of ag / na
+  uint32_t sh[12];                                         // ObsData 16128..16175: phase, res, shop
+  uint32_t d[28];                                          // DeckObs of ag
+  Heads sel, sta, stn;                                     // selected / stored(ag) / stored(na)
+  bool moved;
+  uint4 g2;                                                // map bounds + locations (moves only)
+
+  DEV uint32_t n_players() const { return g1x & 0xffu; }
+  DEV uint32_t done() const { return g1x >> 24; }
+  DEV uint32_t agent() const { return g1y & 0xffu; }
+  DEV uint32_t n_in_market() const { return (g1y >> 8) & 0xffu; }
+  DEV void set_done(uint32_t v) { g1x = (g1x & 0x00ffffffu) | (v << 24); }
+  DEV void set_agent(uint32_t v) { g1y = (g1y & ~0xffu) | (v & 0xffu); }
+  DEV void set_n_in_market(uint32_t v) { g1y = (g1y & ~0xff00u) | ((v & 0xffu) << 8); }
+  DEV uint32_t shop_byte(int k) const {                   // dynamic k: select, no indexed registers
+    const int q = 4 + (k >> 2);
+    uint32_t w = 0;
 #pragma unroll
-  for (int q = 0; q < 6; q++) { d[q] = dk32[q]; x[q] = dk32[21 + q]; }
-  uint32_t nd = P.n_in_draw;
-#pragma unroll
-  for (int k = 0; k < COG_N_CARDTYPES; k++) {
-    const uint32_t v = byte_of(x, k);                      // discard byte 84+k == x byte k
-    put_byte(d, k, byte_of(d, k) + v);
-    nd += v;
-    put_byte(x, k, 0u);
+    for (int x = 4; x < 9; x++) w = x == q ? sh[x] : w;
+    return (w >> (8 * (k & 3))) & 0xffu;
   }
-  P.n_in_draw = (uint8_t)nd;
-#pragma unroll
-  for (int q = 0; q < 6; q++) { dk32[q] = d[q]; dk32[21 + q] = x[q]; }
-}
 
-// hand[k] > 0 for k < 21 as a bitset (hand = bytes 21..41 = dwords 5..10)
-DEV uint32_t hand_bits(const uint32_t *dk32) {
-  uint32_t w[6];
-#pragma unroll
-  for (int q = 0; q < 6; q++) w[q] = dk32[5 + q];
-  uint32_t h = 0;
-#pragma unroll
-  for (int k = 0; k < COG_N_CARDTYPES; k++) h |= (byte_of(w, COG_DECK_HAND + k - 20) != 0u ? 1u : 0u) << k;
-  return h;
-}
-DEV void fast_enable_playing(const uint32_t *dk32, Heads &sel) {   // player.cpp:198-206
-  const uint32_t h = hand_bits(dk32);
-  sel.rem = 1u;
-  sel.play = 1u | (h << 1);
-  sel.spec = 1u | ((h & kSpecialBits) << 1);
-}
+  DEV uint8_t use_cell(const uint2 &cc, int dir) {        // cached lookup (map.cpp:273-275)
+    const uint32_t oob = cc.y >> 24;
+    if ((oob >> dir) & 1u) flags |= F_OOB_LOOKUP;
+    return (uint8_t)(dir < 4 ? (cc.x >> (8 * dir)) : (cc.y >> (8 * (dir - 4))));
+  }
+  DEV uint8_t use_cell_dyn(const uint2 &cc, int dir) {
+    const uint32_t oob = cc.y >> 24;
+    if ((oob >> dir) & 1u) flags |= F_OOB_LOOKUP;
+    const uint64_t v = (uint64_t)cc.x | (uint64_t)cc.y << 32;
+    return (uint8_t)(v >> (8 * dir));
+  }
 
-// Deck::draw (cards.cpp:183-211); the draw-pile scan runs on registers.  n_in_draw equals the
-// sum of draw[] mod 256 (every Deck operation keeps it), so t < n_in_draw always ends inside
-// draw[0..20]; the guard only raises the hazard flag.
-DEV void fast_draw(const Ctx &e, PlayerPriv &P, uint32_t *dk32, Heads &sel, uint32_t &rng, uint8_t n) {
-  if (P.n_in_draw < n) fast_move_discard_to_draw(dk32, P);
-  if (n > P.n_in_draw) n = P.n_in_draw;
-  if (!n) return;
-  uint32_t d[6];
-#pragma unroll
-  for (int q = 0; q < 6; q++) d[q] = dk32[q];
-  for (int i = 0; i < n; i++) {
-    uint32_t t = uid(rng, P.n_in_draw);
-    int c = COG_N_CARDTYPES;
+  // Deck::discard_all_active + discard_all_played (cards.cpp:219-232)
+  DEV void discard_all() {
 #pragma unroll
     for (int k = 0; k < COG_N_CARDTYPES; k++) {
-      const uint32_t v = byte_of(d, k);
-      if (c == COG_N_CARDTYPES) {
-        if (t >= v) t -= v;
-        else c = k;
+      const uint32_t a = dk_get(d, COG_DECK_ACTIVE + k), p = dk_get(d, COG_DECK_PLAYED + k);
+      dk_put(d, COG_DECK_DISCARD + k, dk_get(d, COG_DECK_DISCARD + k) + a + p);
+      dk_put(d, COG_DECK_ACTIVE + k, 0u);
+      dk_put(d, COG_DECK_PLAYED + k, 0u);
+    }
+  }
+  // Deck::move_discard_to_draw (cards.cpp:234-240)
+  DEV void move_discard_to_draw() {
+    uint32_t nd = P.n_in_draw;
+#pragma unroll
+    for (int k = 0; k < COG_N_CARDTYPES; k++) {
+      const uint32_t v = dk_get(d, COG_DECK_DISCARD + k);
+      dk_put(d, COG_DECK_DRAW + k, dk_get(d, COG_DECK_DRAW + k) + v);
+      nd += v;
+      dk_put(d, COG_DECK_DISCARD + k, 0u);
+    }
+    P.n_in_draw = nd & 0xffu;
+  }
+  DEV uint32_t hand_bits() const {
+    uint32_t h = 0;
+#pragma unroll
+    for (int k = 0; k < COG_N_CARDTYPES; k++) h |= (dk_get(d, COG_DECK_HAND + k) != 0u ? 1u : 0u) << k;
+    return h;
+  }
+  DEV void enable_playing() {                              // player.cpp:198-206
+    const uint32_t h = hand_bits();
+    sel.rem = 1u;
+    sel.play = 1u | (h << 1);
+    sel.spec = 1u | ((h & kSpecialBits) << 1);
+  }
+  // Deck::draw (cards.cpp:183-211); n_in_draw == sum(draw[]) mod 256 (every Deck operation
+  // keeps it), so the scan ends inside the pile; the guard only raises the hazard flag
+  DEV void draw(uint32_t n) {
+    if (P.n_in_draw < n) move_discard_to_draw();
+    if (n > P.n_in_draw) n = P.n_in_draw;
+    for (uint32_t i = 0; i < n; i++) {
+      const uint32_t t = uid(rng, P.n_in_draw);
+      uint32_t c = pile_scan<COG_DECK_DRAW>(d, t);
+      if (c >= COG_N_CARDTYPES) {
+        flags |= F_SCAN_OVER;
+        c = COG_N_CARDTYPES - 1;
       }
+      pile_add<COG_DECK_DRAW>(d, (int)c, 0xffu);
+      P.n_in_draw = (P.n_in_draw - 1) & 0xffu;
+      pile_add<COG_DECK_HAND>(d, (int)c, 1u);
+      sel.play |= 1u << (c + 1);
+      sel.spec = set_bit(sel.spec, (int)c + 1, is_special((int)c));
     }
-    if (c == COG_N_CARDTYPES) {                            // unreachable (see above)
-      e.pv->flags |= F_SCAN_OVER;
-      c = COG_N_CARDTYPES - 1;
+    P.n_in_hand = (P.n_in_hand + n) & 0xffu;
+  }
+  // card c leaves the hand (Deck::activate / play_immediate / remove_immediate, cards.cpp:242-290)
+  DEV void leave_hand(int c, bool rem_rule) {
+    const uint32_t prev = pile_get<COG_DECK_HAND>(d, c);
+    pile_add<COG_DECK_HAND>(d, c, 0xffu);
+    P.n_in_hand = (P.n_in_hand - 1) & 0xffu;
+    const uint32_t b = 1u << (c + 1);
+    bool pl = prev > 1;
+    if (rem_rule) {
+      if (!pl) sel.rem &= ~b;
+      pl = pl && (sel.play & b);
     }
+    sel.play = pl ? (sel.play | b) : (sel.play & ~b);
+    sel.spec = (pl && is_special(c)) ? (sel.spec | b) : (sel.spec & ~b);
+  }
+  // Player::cards_from_active (player.cpp:85-131): n random cards leave the active pile; the
+  // reference's scan (cards.cpp:196-201) may run past the pile on an inconsistent deck
+  DEV void take_from_active(uint32_t n, bool discard) {
+    const uint32_t avail = P.n_active;
+    if (n > avail) {
+      if (discard) flags |= F_Q24_CLAMP;
+      n = avail;
+    }
+    for (uint32_t i = 0; i < n; i++) {
+      const uint32_t t = uid(rng, avail - i);
+      uint32_t s = 0, c = 0;
 #pragma unroll
-    for (int q = 0; q < 6; q++)
-      if (q == (c >> 2)) d[q] -= 1u << (8 * (c & 3));      // draw[c] >= 1: no borrow
-    P.n_in_draw--;
-    e.dka[COG_DECK_HAND + c]++;
-    sel.play |= 1u << (c + 1);
-    sel.spec = set_bit(sel.spec, c + 1, is_special(c));
+      for (int k = COG_DECK_ACTIVE; k < 105; k++) {
+        s += dk_get(d, k);
+        c += s <= t ? 1u : 0u;
+      }
+      if (COG_DECK_ACTIVE + c >= 105) flags |= F_SCAN_OVER;
+      P.n_active = (P.n_active - 1) & 0xffu;
+      dk_addv<COG_DECK_ACTIVE, 105>(d, COG_DECK_ACTIVE + (int)c, 0xffu);
+      if (discard) dk_addv<COG_DECK_DISCARD, COG_DECK_DISCARD + 20>(d, COG_DECK_DISCARD + (int)c, 1u);
+    }
   }
+  // movement mask bits 1..6 (map.cpp:369-387) + bit 0, from a player's cached neighbourhood
+  DEV uint32_t move_bits(const uint2 &cc, float r0, float r1, float r2, uint32_t n_active) {
+    uint32_t m = 1u;
 #pragma unroll
-  for (int q = 0; q < 5; q++) dk32[q] = d[q];
-  e.dka[20] = (uint8_t)byte_of(d, 20);                     // bytes 21..23 are hand[0..2]
-  P.n_in_hand = (uint8_t)(P.n_in_hand + n);
-}
-
-// bytes 66..91 (move[0..6], get_from_shop[0..18]) of a stored mask from two bitsets
-DEV void put_move_shop(uint32_t *st32, uint32_t move, uint32_t shop) {
-  const uint32_t v = move | (shop << 7);
-  st32[16] = (st32[16] & 0xffffu) | ((v & 1u) << 16) | (((v >> 1) & 1u) << 24);
+    for (int dir = 1; dir < 7; dir++) {
+      const uint32_t c = use_cell(cc, dir);
+      const uint32_t req = COG_HEX_REQ(c), n = COG_HEX_N(c);
+      const float r = req == 0 ? r0 : (req == 1 ? r1 : r2);
+      const bool filled = req >= COG_REQ_DISCARD ? n_active > n : r >= (float)n;
+      if (req != COG_REQ_NULL && filled) m |= 1u << dir;
+    }
+    return m;
+  }
+  // shop mask bits 1..18 (cards.cpp:109-121) + bit 0
+  DEV uint32_t shop_avail() const {
+    uint32_t nz = 0;
 #pragma unroll
-  for (int q = 0; q < 6; q++) st32[17 + q] = expand4((v >> (2 + 4 * q)) & 0xfu);
-}
-
-DEV uint8_t use_cell(const Ctx &e, const uint8_t *cc, int d) {   // a lookup of the cached cell d
-  if ((cc[7] >> d) & 1u) e.pv->flags |= F_OOB_LOOKUP;
-  return cc[d];
-}
-// movement mask bits 1..6 (map.cpp:369-387) + bit 0, from a player's cached neighbourhood
-DEV uint32_t move_bits(const Ctx &e, const uint8_t *cc, float r0, float r1, float r2, uint8_t n_active) {
-  uint32_t m = 1u;
+    for (int q = 0; q < 5; q++) nz |= bools4(sh[4 + q]) << (4 * q);
+    return n_in_market() < COG_MKT_SLOTS ? (nz & 0x3ffffu) : (in_market & 0x3ffffu);
+  }
+  DEV uint32_t shop_bits(float coins) const {
+    const uint32_t afford = (coins > 1.f ? kCostMask1 : 0u) | (coins > 2.f ? kCostMask2 : 0u) |
+                            (coins > 3.f ? kCostMask3 : 0u) | (coins > 4.f ? kCostMask4 : 0u) |
+                            (coins > 5.f ? kCostMask5 : 0u);
+    return 1u | ((shop_avail() & afford) << 1);
+  }
+  // special actions (cards.cpp:8-36, the remove lambda environment.cpp:156-158) on the stored
+  // mask `m` of the current agent and the selected mask, for the acting player (:183-186)
+  DEV void apply_special(int special, Heads &m) {
+    switch (special) {
+      case COG_SPECIAL_DRAW2:
+      case COG_SPECIAL_DRAW3: draw(special == COG_SPECIAL_DRAW2 ? 2u : 3u); break;
+      case COG_SPECIAL_DRAW1_REMOVE1:
+      case COG_SPECIAL_DRAW2_REMOVE2: {
+        const uint32_t k = special == COG_SPECIAL_DRAW1_REMOVE1 ? 1u : 2u;
+        draw(k);
+        P.n_removes = k;
+        m.rem = m.play;                                    // mask.remove = mask.play
+        sel.play = 1u;                                     // disable_playing
+        sel.spec = 1u;
+        m.shop &= 1u;                                      // shop_mask(0): nothing affordable
+      } break;
+      case COG_SPECIAL_TRANSMIT: {
+        m.move = 1u;
+        sel.play = 1u;
+        sel.spec = 1u;
+        uint32_t nz = 0;
 #pragma unroll
-  for (int d = 1; d < 7; d++) {
-    const uint8_t c = use_cell(e, cc, d);
-    const int req = COG_HEX_REQ(c);
-    const uint32_t n = COG_HEX_N(c);
-    const float r = req == 0 ? r0 : (req == 1 ? r1 : r2);
-    const bool filled = req >= COG_REQ_DISCARD ? n_active > n : r >= (float)n;
-    if (req != COG_REQ_NULL && filled) m |= 1u << d;
-  }
-  return m;
-}
-// shop mask bits 1..18 (cards.cpp:109-121) + bit 0
-DEV uint32_t shop_bits(const Ctx &e, float coins) {
-  const bool few = e.pv->n_in_market < COG_MKT_SLOTS;
-  const uint32_t im = e.pv->in_market;
-  uint32_t m = 1u;
+        for (int q = 0; q < 5; q++) nz |= bools4(sh[4 + q]) << (4 * q);
+        m.shop = (m.shop & 1u) | ((nz & 0x3ffffu) << 1);
+        P.next_card_free = 1;
+      } break;
+      case COG_SPECIAL_NATIVE: {
+        uint32_t mb = m.move & 1u;
 #pragma unroll
-  for (int i = 0; i < COG_N_SHOP; i++) {
-    const bool ok = few ? e.sh[SH_SHOP + i] > 0 : ((im >> i) & 1u);
-    if (ok && coins > (float)kCards[kShopTypes[i]].cost) m |= 1u << (i + 1);
+        for (int dir = 1; dir < 7; dir++)                  // movement_mask with 100 of everything
+          if (COG_HEX_REQ(use_cell(cells_a, dir)) != COG_REQ_NULL) mb |= 1u << dir;
+        m.move = mb;
+        P.next_move_free = 1;
+        sel.play = 1u;
+        sel.spec = 1u;
+        m.shop &= 1u;
+      } break;
+      case COG_SPECIAL_SHOP_OFF: m.shop &= 1u; break;
+      default: break;
+    }
   }
-  return m;
-}
-DEV uint32_t gran(int byte) { return 1u << (byte >> 4); }   // 16-B granule bit of a record byte
-
-// Player::cards_from_active (player.cpp:85-131): n random cards leave the active pile
-DEV void take_from_active(const Ctx &e, PlayerPriv &P, uint8_t n, bool discard) {
-  uint8_t *d = e.dka;
-  const uint8_t avail = P.n_active;
-  if (n > avail) {
-    if (discard) e.pv->flags |= F_Q24_CLAMP;
-    n = avail;
-  }
-  uint32_t rng = e.pv->rng;
-  for (uint8_t i = 0; i < n; i++) {
-    const uint32_t t = uid(rng, (uint32_t)(avail - i));
-    const int c = scan(e, d, COG_DECK_ACTIVE, t);
-    P.n_active--;
-    d[COG_DECK_ACTIVE + c]--;
-    if (discard) d[COG_DECK_DISCARD + c]++;
-  }
-  e.pv->rng = rng;
-}
-
-// card c leaves the hand (Deck::activate / play_immediate / remove_immediate, cards.cpp:242-290)
-// and the selected mask's play / special / remove bits of c follow (rem_rule: remove_immediate)
-DEV void leave_hand(const Ctx &e, PlayerPriv &P, Heads &sel, int c, bool rem_rule) {
-  const uint8_t prev = e.dka[COG_DECK_HAND + c];
-  e.dka[COG_DECK_HAND + c] = (uint8_t)(prev - 1);
-  P.n_in_hand--;
-  const uint32_t b = 1u << (c + 1);
-  bool pl = prev > 1;
-  if (rem_rule) {
-    if (!pl) sel.rem &= ~b;
-    pl = pl && (sel.play & b);
-  }
-  sel.play = pl ? (sel.play | b) : (sel.play & ~b);
-  sel.spec = (pl && is_special(c)) ? (sel.spec | b) : (sel.spec & ~b);
-}
-
-struct Plan {                         // 16-B granules to store back, per staged record
-  uint32_t pv, sh, dk, st, stn;
 };
 
-// special actions (cards.cpp:8-36, the remove lambda environment.cpp:156-158) on the stored mask
-// `stc` of the CURRENT agent and the selected mask, for the ACTING player P (:183-186)
-DEV void apply_special(const Ctx &e, int special, int ag, PlayerPriv &P, Heads &sel, uint8_t *stc) {
-  Heads m = heads_from(stc);
-  switch (special) {
-    case COG_SPECIAL_DRAW2:
-    case COG_SPECIAL_DRAW3: {
-      uint32_t rng = e.pv->rng;
-      fast_draw(e, P, reinterpret_cast<uint32_t *>(e.dka), sel, rng, special == COG_SPECIAL_DRAW2 ? 2 : 3);
-      e.pv->rng = rng;
-    } break;
-    case COG_SPECIAL_DRAW1_REMOVE1:
-    case COG_SPECIAL_DRAW2_REMOVE2: {
-      const uint8_t k = special == COG_SPECIAL_DRAW1_REMOVE1 ? 1 : 2;
-      uint32_t rng = e.pv->rng;
-      fast_draw(e, P, reinterpret_cast<uint32_t *>(e.dka), sel, rng, k);
-      e.pv->rng = rng;
-      P.n_removes = k;
-      m.rem = m.play;                                      // mask.remove = mask.play
-      sel.play = 1u;                                       // disable_playing
-      sel.spec = 1u;
-      m.shop &= 1u;                                        // shop_mask(0): nothing affordable
-    } break;
-    case COG_SPECIAL_TRANSMIT: {
-      m.move = 1u;
-      sel.play = 1u;
-      sel.spec = 1u;
-      uint32_t sb = m.shop & 1u;
+// the mover's new neighbourhood (load_cells on registers + the compact code grid)
+DEV uint2 cells_at(const uint8_t *cgrid, const uint4 &g2, int lx, int ly) {
+  const int minx = (int8_t)(g2.x & 0xffu), miny = (int8_t)((g2.x >> 8) & 0xffu);
+  const int dimx = g2.y & 0xffu, dimy = (g2.y >> 8) & 0xffu;
+  uint32_t v[7], oob = 0;
 #pragma unroll
-      for (int i = 0; i < COG_N_SHOP; i++)
-        if (e.sh[SH_SHOP + i] > 0) sb |= 1u << (i + 1);
-      m.shop = sb;
-      P.next_card_free = 1;
-    } break;
-    case COG_SPECIAL_NATIVE: {
-      const uint8_t *cc = e.pv->cells[ag];
-      uint32_t mb = m.move & 1u;
-#pragma unroll
-      for (int d = 1; d < 7; d++)                          // movement_mask with 100 of everything
-        if (COG_HEX_REQ(use_cell(e, cc, d)) != COG_REQ_NULL) mb |= 1u << d;
-      m.move = mb;
-      P.next_move_free = 1;
-      sel.play = 1u;
-      sel.spec = 1u;
-      m.shop &= 1u;
-    } break;
-    case COG_SPECIAL_SHOP_OFF: m.shop &= 1u; break;
-    default: break;
+  for (int dir = 0; dir < 7; dir++) {
+    const int ix = lx + c_dirs[dir][0] / 2 - minx + 1, iy = ly + c_dirs[dir][1] / 2 - miny + 1;
+    const bool out_ = ix < 0 || iy < 0 || ix >= dimx || iy >= dimy;
+    const bool ring = ix >= COG_GRID || iy >= COG_GRID;
+    const int cx = min(max(ix, 0), COG_GRID - 1), cy = min(max(iy, 0), COG_GRID - 1);
+    const uint32_t c = cgrid[cx * COG_GRID + cy];
+    v[dir] = (out_ || ring || !c) ? (uint32_t)COG_HEX_MOUNTAIN : c;
+    oob |= (out_ ? 1u : 0u) << dir;
   }
-  heads_to(m, reinterpret_cast<uint32_t *>(stc));
+  return make_uint2(v[0] | v[1] << 8 | v[2] << 16 | v[3] << 24, v[4] | v[5] << 8 | v[6] << 16 | oob << 24);
 }
 
-// cog_env::step (environment.cpp:91-224) for the acting player a0 == agent, every action kind.
-// State: deck / stored mask of a0, stored mask of na, phase / resources / shop and EnvPriv in
-// the LDS slot; selected mask in `sel` (bitsets).  Returns the granules it modified.
-DEV Plan step_env(const Ctx &e, const uint8_t act[5], Heads &sel, uint8_t *stn, int na) {
-  EnvPriv *pv = e.pv;
-  const int ag = pv->agent;
-  Plan o{0xbu | (1u << (4 + ag)), 0x1u, 0u, 0u, 0u};       // rng/counters, agent/flags, info mirror
-  e.info[COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag] = ++pv->info_steps[ag];   // steps_taken (u8)
-  uint8_t phase = e.sh[0];
+// cog_env::step (environment.cpp:91-224) for the acting player ag == agent, every action kind.
+// Returns true when the episode ends (finish_episode runs on the stored state afterwards).
+DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i, int na) {
+  const int ag = (int)R.agent();
+  PState &P = R.P;
+  const uint32_t info = ((R.info_steps >> (8 * ag)) + 1u) & 0xffu;   // Info steps_taken (u8)
+  R.info_steps = (R.info_steps & ~(0xffu << (8 * ag))) | (info << (8 * ag));
+  s.info[i * COG_INFO_BYTES + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag] = (uint8_t)info;
+  uint32_t phase = R.sh[0] & 0xffu;
   if (phase == COG_PHASE_INACTIVE) phase = COG_PHASE_MOVEMENT;
-  PlayerPriv &P = pv->pl[ag];
-  P.steps_taken++;
-  float *res3 = res(e);
-  float r0 = res3[0], r1 = res3[1], r2 = res3[2];
-  uint8_t *d = e.dka;
-  uint32_t *dk32 = reinterpret_cast<uint32_t *>(d);
-  const uint8_t a_play = act[0], a_special = act[1], a_remove = act[2], a_move = act[3], a_shop = act[4];
+  P.steps_taken = (P.steps_taken + 1) & 0xffu;
+  float r0 = __uint_as_float(R.sh[1]), r1 = __uint_as_float(R.sh[2]), r2 = __uint_as_float(R.sh[3]);
+  const int a_play = act[0], a_special = act[1], a_remove = act[2], a_move = act[3], a_shop = act[4];
   int special = COG_SPECIAL_NONE;
-  bool moved = false;
   if (a_play) {                                            // Player::play_card (player.cpp:45-60)
     const int c = a_play - 1;
     if (phase == COG_PHASE_MOVEMENT) {
-      r0 = (float)c_cards[c].res[0]; r1 = (float)c_cards[c].res[1]; r2 = (float)c_cards[c].res[2];
+      r0 = (float)cardf(kRes0, c); r1 = (float)cardf(kRes1, c); r2 = (float)cardf(kRes2, c);
     } else if (phase == COG_PHASE_BUYING) {
-      const uint8_t coin = c_cards[c].res[2];
+      const uint32_t coin = cardf(kRes2, c);
       r2 = r2 + (coin > 0 ? (float)coin : 0.5f);
     }
-    leave_hand(e, P, sel, c, false);                       // Deck::activate
-    d[COG_DECK_ACTIVE + c]++;
-    P.n_active++;
-    P.idx_last = (uint8_t)c;
-    o.dk |= gran(COG_DECK_HAND + c) | gran(COG_DECK_ACTIVE + c);
+    R.leave_hand(c, false);                                // Deck::activate
+    pile_add<COG_DECK_ACTIVE>(R.d, c, 1u);
+    P.n_active = (P.n_active + 1) & 0xffu;
+    P.idx_last = (uint32_t)c;
   } else if (a_special) {                                  // play_special (environment.cpp:108-114)
     const int c = a_special - 1;
-    const bool single = c_cards[c].single_use;
-    leave_hand(e, P, sel, c, single);                      // remove_immediate / play_immediate
-    if (!single) {
-      d[COG_DECK_PLAYED + c]++;
-      o.dk |= gran(COG_DECK_PLAYED + c);
-    }
-    o.dk |= gran(COG_DECK_HAND + c);
-    special = c_cards[c].special;
+    const bool single = cardf(kSingle, c) != 0u;
+    R.leave_hand(c, single);                               // remove_immediate / play_immediate
+    if (!single) pile_add<COG_DECK_PLAYED>(R.d, c, 1u);
+    special = (int)cardf(kSpecial, c);
   } else if (a_move) {                                     // move (environment.cpp:115-127)
-    const uint8_t c = use_cell(e, pv->cells[ag], a_move);
-    pv->locx[ag] = (int8_t)(pv->locx[ag] + c_dirs[a_move][0] / 2);
-    pv->locy[ag] = (int8_t)(pv->locy[ag] + c_dirs[a_move][1] / 2);
+    const uint32_t c = R.use_cell_dyn(R.cells_a, a_move);
+    R.g2 = reinterpret_cast<const uint4 *>(s.priv + i)[2]; // map bounds + locations
+    const int lx = (int8_t)((R.g2.z >> (8 * ag)) & 0xffu) + c_dirs[a_move][0] / 2;
+    const int ly = (int8_t)((R.g2.w >> (8 * ag)) & 0xffu) + c_dirs[a_move][1] / 2;
+    R.g2.z = (R.g2.z & ~(0xffu << (8 * ag))) | (((uint32_t)lx & 0xffu) << (8 * ag));
+    R.g2.w = (R.g2.w & ~(0xffu << (8 * ag))) | (((uint32_t)ly & 0xffu) << (8 * ag));
     if (!P.next_move_free) {                               // Player::handle_requirement (:141-162)
-      const int req = COG_HEX_REQ(c);
-      const uint8_t n = COG_HEX_N(c);
+      const uint32_t req = COG_HEX_REQ(c), n = COG_HEX_N(c);
       if (req < 3) {
         const float left = (req == 0 ? r0 : req == 1 ? r1 : r2) - (float)n;
         r0 = req == 0 ? left : 0.f;
         r1 = req == 1 ? left : 0.f;
         r2 = req == 2 ? left : 0.f;
         if (!P.mip) {                                      // Deck::play_last_activated
-          const int l = P.idx_last;
-          P.n_active--;
-          d[COG_DECK_ACTIVE + l]--;
-          o.dk |= gran(COG_DECK_ACTIVE + l);
-          if (!c_cards[l].single_use) {
-            d[COG_DECK_PLAYED + l]++;
-            o.dk |= gran(COG_DECK_PLAYED + l);
-          }
+          const int l = (int)P.idx_last;
+          P.n_active = (P.n_active - 1) & 0xffu;
+          dk_addv<COG_DECK_ACTIVE, 105>(R.d, COG_DECK_ACTIVE + l, 0xffu);
+          if (!cardf(kSingle, l)) dk_addv<COG_DECK_PLAYED, 105>(R.d, COG_DECK_PLAYED + l, 1u);
           P.mip = 1;
         }
       } else if (req == COG_REQ_REMOVE || req == COG_REQ_DISCARD) {
-        take_from_active(e, P, n, req == COG_REQ_DISCARD);
+        R.take_from_active(n, req == COG_REQ_DISCARD);
         r0 = r1 = r2 = 0.f;
         P.mip = 0;
-        o.dk = 0x7fu;
       }
     } else {
       P.next_move_free = 0;
-      fast_enable_playing(dk32, sel);
+      R.enable_playing();
     }
     P.n_movements++;
     P.has_won = COG_HEX_END(c);
-    moved = true;
-    o.pv |= 0x4u;                                          // player locations
+    R.moved = true;
   } else {
     P.next_move_free = 0;
     if (a_shop) {                                          // Shop::get_card (cards.cpp:123-142)
       const int k = a_shop - 1;
-      const int type = kShopTypes[k];
+      const int ty = shop_type(k);
       const uint32_t bit = 1u << k;
+      uint32_t nim = R.n_in_market();
       if (!P.next_card_free) {
-        pv->n_in_market = (uint8_t)(pv->n_in_market + ((pv->in_market & bit) ? 0 : 1));
-        pv->in_market |= bit;
+        nim = (nim + ((R.in_market & bit) ? 0u : 1u)) & 0xffu;
+        R.in_market |= bit;
       }
-      const uint8_t left = (uint8_t)(e.sh[SH_SHOP + k] - 1);
-      e.sh[SH_SHOP + k] = left;
-      if (!left && (pv->in_market & bit)) {
-        pv->in_market &= ~bit;
-        pv->n_in_market--;
+      const uint32_t left = (R.shop_byte(k) - 1u) & 0xffu;
+      const int q = 4 + (k >> 2), sh8 = 8 * (k & 3);
+#pragma unroll
+      for (int w = 4; w < 9; w++)
+        if (w == q) R.sh[w] = (R.sh[w] & ~(0xffu << sh8)) | (left << sh8);
+      if (!left && (R.in_market & bit)) {
+        R.in_market &= ~bit;
+        nim = (nim - 1u) & 0xffu;
       }
+      R.set_n_in_market(nim);
       if (!P.next_card_free) {
-        r2 = r2 - (float)c_cards[type].cost;
-        phase = (uint8_t)((phase + 1) % 3);
+        r2 = r2 - (float)cardf(kCost, ty);
+        phase = (phase + 1) % 3;
       }
-      d[COG_DECK_DISCARD + type]++;
-      P.n_added_cards++;
-      o.dk |= gran(COG_DECK_DISCARD + type);
-      o.sh |= gran(SH_SHOP + k);
+      pile_add<COG_DECK_DISCARD>(R.d, ty, 1u);
+      P.n_added_cards = (P.n_added_cards + 1) & 0xffu;
     } else if (a_remove) {
       const int c = a_remove - 1;
-      leave_hand(e, P, sel, c, true);                      // Deck::remove_immediate
-      o.dk |= gran(COG_DECK_HAND + c);
-      P.n_removes--;
-      if (!P.n_removes) fast_enable_playing(dk32, sel);
+      R.leave_hand(c, true);                               // Deck::remove_immediate
+      P.n_removes = (P.n_removes - 1) & 0xffu;
+      if (!P.n_removes) R.enable_playing();
       else special = COG_SPECIAL_SHOP_OFF;
     } else {                                               // pass: next phase
-      phase = (uint8_t)((phase + 1) % 3);
+      phase = (phase + 1) % 3;
       if (P.n_removes > 0) {
         P.n_removes = 0;
-        fast_enable_playing(dk32, sel);
+        R.enable_playing();
       }
     }
     if (P.next_card_free) {
       P.next_card_free = 0;
-      fast_enable_playing(dk32, sel);
+      R.enable_playing();
     }
   }
-  STAMP_AT(3);
   if (P.mip && !a_move) {                                  // the move HEAD, whatever was taken
     P.mip = 0;
     r0 = r1 = r2 = 0.f;
   }
-  int cur = ag;
+  bool cur_is_ag = true;
   if (P.has_won || phase == COG_PHASE_INACTIVE) {          // maybe_end_turn -> next_agent
     P.n_active = 0;                                        // Player::end_turn (player.cpp:170-180)
-    fast_discard_all(dk32);
+    R.discard_all();
     const int n_draw = COG_HAND_SIZE - (int)P.n_in_hand;
-    if (n_draw > 0) {
-      uint32_t rng = pv->rng;
-      fast_draw(e, P, dk32, sel, rng, (uint8_t)n_draw);
-      pv->rng = rng;
+    if (n_draw > 0) R.draw((uint32_t)n_draw);
+    R.sta = R.sel;                                         // save_actionmask
+    R.set_agent((uint32_t)na);
+    if (na == ag) R.sel = R.sta;                           // load_actionmask
+    else {
+      R.sel = R.stn;
+      cur_is_ag = false;
     }
-    heads_to(sel, reinterpret_cast<uint32_t *>(e.sta));  // save_actionmask
-    o.dk = 0x7fu;
-    o.st = 0x3fu;
-    pv->agent = (uint8_t)na;
-    sel = heads_from(na == ag ? e.sta : stn);             // load_actionmask
     r0 = r1 = r2 = 0.f;
-    pv->turn_counter++;
-    cur = na;
+    R.turn_counter++;
   }
-  STAMP_AT(4);
-  e.sh[0] = phase;
-  res3[0] = r0; res3[1] = r1; res3[2] = r2;
-  if (moved) {                                             // the mover's new neighbourhood
-    load_cells(e, ag);
-    o.pv |= 1u << (8 + ag / 2);
+  R.sh[0] = (R.sh[0] & ~0xffu) | phase;
+  R.sh[1] = __float_as_uint(r0); R.sh[2] = __float_as_uint(r1); R.sh[3] = __float_as_uint(r2);
+  if (R.moved) {                                           // the mover's new neighbourhood
+    R.cells_a = cells_at(s.cgrid + i * COG_CELLS, R.g2, (int8_t)((R.g2.z >> (8 * ag)) & 0xffu),
+                         (int8_t)((R.g2.w >> (8 * ag)) & 0xffu));
+    if (na == ag) R.cells_n = R.cells_a;
   }
-  STAMP_AT(5);
-  const uint8_t *cc = pv->cells[cur];
-  uint8_t *stc = cur == ag ? e.sta : stn;
+  const uint2 cc = cur_is_ag ? R.cells_a : R.cells_n;
+  Heads &stc = cur_is_ag ? R.sta : R.stn;
   uint32_t mv = 1u, sp = 1u;                               // update_observation (:252-279)
-  if (phase == COG_PHASE_MOVEMENT) mv = move_bits(e, cc, r0, r1, r2, pv->pl[cur].n_active);
-  else if (phase == COG_PHASE_BUYING) sp = shop_bits(e, r2);
-  put_move_shop(reinterpret_cast<uint32_t *>(stc), mv, sp);
-  STAMP_AT(6);
-  uint32_t st_dirty = 0x30u;
+  if (phase == COG_PHASE_MOVEMENT) mv = R.move_bits(cc, r0, r1, r2, cur_is_ag ? P.n_active : R.na_active);
+  else if (phase == COG_PHASE_BUYING) sp = R.shop_bits(r2);
+  stc.move = mv;
+  stc.shop = sp;
   if (special != COG_SPECIAL_NONE) {
-    apply_special(e, special, ag, P, sel, stc);
-    st_dirty = 0x3fu;
-    o.dk = 0x7fu;
-  } else {
-    const uint8_t c = use_cell(e, cc, 0);                  // done check (:187)
-    if (COG_HEX_END(c) || pv->turn_counter >= pv->max_steps) finish_episode(e);
+    R.apply_special(special, stc);
+    return false;
   }
-  STAMP_AT(7);
-  if (cur == ag) o.st |= st_dirty;
-  else o.stn |= st_dirty;
-  return o;
+  const uint32_t c0 = R.use_cell(cc, 0);                   // done check (:187)
+  return COG_HEX_END(c0) || R.turn_counter >= R.max_steps;
 }
 
-// Cooperative staging helpers.  Item it = k * 64 + lane of a record of G granules belongs to env
-// it / G, granule it % G.  Loads clamp the env to the block's last valid one (duplicate reads,
-// no branches); stores are predicated on the store plan.
-template <int G>
-DEV int item_env(int k, int lane) { return (k * 64 + lane) / G; }
-template <int G>
-DEV int item_gran(int k, int lane) { return (k * 64 + lane) % G; }
-template <int G>
-constexpr int n_items() { return (G * kWaveEnvs + 63) / 64; }
-
-// One step of the wave's 64 envs (each optionally preceded by sampling its action).
-// act_in: actions of the host API path (nullptr in the fused runner path).
-// Latency plan (one wave per SIMD at the benchmark's size, so nothing hides a stall):
-//   round 1 loads (state at fixed addresses) -> LDS -> round 2 loads (agent-dependent records)
-//   issued -> sampling on the round-1 state while they fly -> LDS -> game logic -> all LDS
-//   reads of the store phase batched -> predicated 16-B stores.
-DEV void wave_step(const DevState &s, uint32_t *slots, const uint8_t *act_in, int mask_source,
-                   uint32_t *rngs, uint8_t *actions_out) {
-  const int lane = threadIdx.x;
-  const size_t base = (size_t)blockIdx.x * kWaveEnvs;
-  const int nv = s.n - base < (size_t)kWaveEnvs ? (int)(s.n - base) : kWaveEnvs;
-  auto slot_of = [&](int e) { return slots + e * kSlotWords; };
-  auto cl = [&](int e) { return e < nv ? e : nv - 1; };
-  auto obs_of = [&](int e) { return s.obs + (base + e) * COG_OBS_BYTES; };
-  auto player_of = [&](int e, int p) { return obs_of(e) + COG_OBS_PLAYER0 + COG_OBS_PLAYER_STRIDE * p; };
-  STAMP(s, 0);
-  const size_t i = base + (size_t)cl(lane);
-  const bool live = lane < nv;
-
-  // round 1: EnvPriv (10 granules), selected mask (6), phase/resources/shop (3), sampler rng
-  {
-    constexpr int KA = n_items<kPvG>(), KB = n_items<6>(), KC = n_items<3>();
-    uint4 a[KA], b[KB], c[KC];
+// One env per work-item: load (two rounds), [sample], step, store what changed, [auto-reset].
+// SRC: MASK_SELECTED / MASK_STORED (runner, sampling fused) or MASK_EXTERNAL (host actions).
+template <int SRC>
+DEV bool env_step_lane(const DevState &s, size_t i, const uint8_t *act_in, uint32_t *rngs, uint8_t *actions_out) {
+  RegEnv R;
+  const uint4 *pv4 = reinterpret_cast<const uint4 *>(s.priv + i);
+  uint8_t *ob = s.obs + i * COG_OBS_BYTES;
+  // round 1: records at fixed addresses
+  const uint4 g0 = pv4[0], g1 = pv4[1];
+  const uint32_t info_steps = reinterpret_cast<const uint32_t *>(pv4 + 3)[0];
+  const uint4 hsel = s.heads[5 * i];
+  const uint4 sh0 = reinterpret_cast<const uint4 *>(ob + COG_OBS_PHASE)[0];
+  const uint4 sh1 = reinterpret_cast<const uint4 *>(ob + COG_OBS_PHASE)[1];
+  const uint4 sh2 = reinterpret_cast<const uint4 *>(ob + COG_OBS_PHASE)[2];
+  uint32_t srng = SRC == MASK_EXTERNAL ? 0u : rngs[i];
+  R.rng = g0.x; R.seed = g0.y; R.max_steps = g0.z; R.turn_counter = g0.w;
+  R.g1x = g1.x; R.g1y = g1.y; R.in_market = g1.z; R.flags = g1.w;
+  R.info_steps = info_steps;
+  R.moved = false;
+  const int ag = (int)R.agent();
+  const int na = ag + 1 >= (int)R.n_players() ? 0 : ag + 1;
+  // round 2: the acting / next player's records
+  const uint4 pla = pv4[4 + ag], pln = pv4[4 + na];
+  R.cells_a = reinterpret_cast<const uint2 *>(pv4 + 8)[ag];
+  R.cells_n = reinterpret_cast<const uint2 *>(pv4 + 8)[na];
+  const uint4 hsta = s.heads[5 * i + 1 + ag], hstn = s.heads[5 * i + 1 + na];
+  uint8_t *deck = ob + COG_OBS_PLAYER0 + COG_OBS_PLAYER_STRIDE * ag;
+  uint4 dk[7];
 #pragma unroll
-    for (int k = 0; k < KA; k++)
-      a[k] = reinterpret_cast<const uint4 *>(s.priv + base + cl(item_env<kPvG>(k, lane)))[item_gran<kPvG>(k, lane)];
-#pragma unroll
-    for (int k = 0; k < KB; k++)
-      b[k] = reinterpret_cast<const uint4 *>(s.sel + (base + cl(item_env<6>(k, lane))) * COG_MASK_BYTES)[item_gran<6>(k, lane)];
-#pragma unroll
-    for (int k = 0; k < KC; k++)
-      c[k] = reinterpret_cast<const uint4 *>(obs_of(cl(item_env<3>(k, lane))) + COG_OBS_PHASE)[item_gran<3>(k, lane)];
-#pragma unroll
-    for (int k = 0; k < KA; k++) lds_put4(slot_of(item_env<kPvG>(k, lane)) + SLOT_PV / 4 + 4 * item_gran<kPvG>(k, lane), a[k]);
-#pragma unroll
-    for (int k = 0; k < KB; k++) lds_put4(slot_of(item_env<6>(k, lane)) + SLOT_SEL / 4 + 4 * item_gran<6>(k, lane), b[k]);
-#pragma unroll
-    for (int k = 0; k < KC; k++) lds_put4(slot_of(item_env<3>(k, lane)) + SLOT_SH / 4 + 4 * item_gran<3>(k, lane), c[k]);
-  }
-  uint32_t rng = act_in ? 0u : rngs[i];
-  __syncthreads();
-
-  // round 2 (addresses depend on the agent): deck + stored mask of a0 (13 granules, skipping the
-  // DeckObs padding granule), stored mask of na (6).  Issued, then the sampler runs on the
-  // round-1 state while they are in flight.
-  uint32_t *slot = slot_of(lane);
-  uint8_t *lds = reinterpret_cast<uint8_t *>(slot);
-  EnvPriv *pv = reinterpret_cast<EnvPriv *>(lds + SLOT_PV);
-  const int a0 = pv->agent;
-  const int na = a0 + 1 >= pv->n_players ? 0 : a0 + 1;
-  const int players = a0 | na << 2;                        // this lane's env: a0, na
-  constexpr int KD = n_items<13>(), KE = n_items<6>();
-  uint4 dk[KD], sn[KE];
-#pragma unroll
-  for (int k = 0; k < KD; k++) {
-    const int e = item_env<13>(k, lane), g = item_gran<13>(k, lane);
-    const int pa = __shfl(players, cl(e)) & 3;
-    dk[k] = reinterpret_cast<const uint4 *>(player_of(cl(e), pa))[g < 7 ? g : g + 1];
-  }
-#pragma unroll
-  for (int k = 0; k < KE; k++) {
-    const int e = item_env<6>(k, lane), g = item_gran<6>(k, lane);
-    const int pn = __shfl(players, cl(e)) >> 2;
-    sn[k] = reinterpret_cast<const uint4 *>(player_of(cl(e), pn) + COG_PD_MASK)[g];
-  }
-  Heads sel = heads_from(lds + SLOT_SEL);
-  uint8_t act[5] = {0, 0, 0, 0, 0};
-  if (act_in) {                                            // host actions: indices past a head
+  for (int k = 0; k < 7; k++) dk[k] = reinterpret_cast<const uint4 *>(deck)[k];
+  // the sampler needs round 1 only: it runs while round 2 is in flight
+  R.sel = heads_of(mbits_of(hsel));
+  uint8_t act[5];
+  if (SRC == MASK_SELECTED) sample_heads(R.sel, srng, act);
+  // unpack round 2
+  R.P = unpack_player(pla);
+  R.na_active = (pln.y >> 16) & 0xffu;
+  R.sta = heads_of(mbits_of(hsta));
+  R.stn = heads_of(mbits_of(hstn));
+  if (SRC == MASK_STORED) sample_heads(R.sta, srng, act);
+  if (SRC == MASK_EXTERNAL) {                              // host actions: indices past a head
     const uint8_t *ai = act_in + i * COG_ACTION_BYTES;     // are the reference's OOB accesses
     const uint8_t top[5] = {COG_N_CARDTYPES, COG_N_CARDTYPES, COG_N_CARDTYPES, 6, COG_N_SHOP};
 #pragma unroll
@@ -1383,140 +1415,108 @@ DEV void wave_step(const DevState &s, uint32_t *slots, const uint8_t *act_in, in
       act[k] = ai[k];
       if (act[k] > top[k]) {
         act[k] = top[k];
-        if (live) pv->flags |= F_BAD_ACTION;
+        R.flags |= F_BAD_ACTION;
       }
     }
-  } else if (mask_source != MASK_STORED) {                 // runner: sample(selected masks)
-    sample_heads(sel, rng, act);
-  }
-#pragma unroll
-  for (int k = 0; k < KD; k++) lds_put4(slot_of(item_env<13>(k, lane)) + SLOT_DK / 4 + 4 * item_gran<13>(k, lane), dk[k]);
-#pragma unroll
-  for (int k = 0; k < KE; k++) lds_put4(slot_of(item_env<6>(k, lane)) + SLOT_STN / 4 + 4 * item_gran<6>(k, lane), sn[k]);
-  __syncthreads();
-  STAMP(s, 1);
-
-  // per-lane game logic on the slot of env `lane`
-  bool enc = false;
-  if (live) {
-    Ctx e;
-    e.ob = s.obs + i * COG_OBS_BYTES;
-    e.sh = lds + SLOT_SH;
-    e.dka = lds + SLOT_DK;
-    e.sta = lds + SLOT_ST;
-    e.a0 = a0;
-    e.sel = lds + SLOT_SEL;
-    e.info = s.info + i * COG_INFO_BYTES;
-    e.rew = s.rew + i * 4;
-    e.pv = pv;
-    e.grid = s.grid + i * (size_t)kGridBytes;
-    e.cgrid = s.cgrid + i * COG_CELLS;
-    e.gs = s.gen + i;
-    e.stamps = s.stamps;
-
-    if (!act_in) {
-      if (mask_source == MASK_STORED) sample_heads(heads_from(e.sta), rng, act);   // runner, stored masks
-      rngs[i] = rng;
-      store_action(actions_out + i * COG_ACTION_BYTES, act);
-    }
-    STAMP(s, 2);
-    Plan o{0x3u, 0u, 0u, 0u, 0u};                          // flags may change (bad action)
-    if (!pv->done) o = step_env(e, act, sel, lds + SLOT_STN, na);
-    STAMP(s, 10);
-    const uint8_t done = pv->done;
-    s.done[i] = done;                                      // dones[i] before the auto-reset
-    if (done) {                                            // vec_environment.h:56-59
-      heads_to(sel, reinterpret_cast<uint32_t *>(e.sel));
-      o = Plan{(1u << kPvG) - 1u, 0x7u, 0x7fu, 0x3fu, 0u}; // na's staged mask is stale now
-      if (!env_reset(e)) {
-        atomicOr(&s.status[0], pv->flags);
-        atomicAdd(&s.status[1], 1u);
-      } else {
-        enc = true;
-        const uint32_t k = atomicAdd(&s.status[2], 1u);
-        if (k < s.n) s.dirty[k] = (uint32_t)i;
-      }
-      sel = heads_from(e.sel);
-    }
-    s.agent[i] = pv->agent;
-    heads_to(sel, slot + SLOT_SEL / 4);
-    slot[SLOT_PLAN / 4] = o.pv | o.sh << 10 | o.dk << 13 | o.st << 20 | o.stn << 26;
-    slot[SLOT_PLAN / 4 + 1] = (uint32_t)a0 | (uint32_t)na << 2;   // records of the ORIGINAL agent
-    STAMP(s, 11);
   } else {
-    slot[SLOT_PLAN / 4] = 0u;                              // lanes past the batch store nothing
+    rngs[i] = srng;
+    store_action(actions_out + i * COG_ACTION_BYTES, act);
   }
-  __syncthreads();
+  const uint4 sh_in[3] = {sh0, sh1, sh2};
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    R.sh[4 * k] = sh_in[k].x; R.sh[4 * k + 1] = sh_in[k].y; R.sh[4 * k + 2] = sh_in[k].z; R.sh[4 * k + 3] = sh_in[k].w;
+  }
+#pragma unroll
+  for (int k = 0; k < 7; k++) {
+    R.d[4 * k] = dk[k].x; R.d[4 * k + 1] = dk[k].y; R.d[4 * k + 2] = dk[k].z; R.d[4 * k + 3] = dk[k].w;
+  }
+  const MBits sel0 = mbits_of(hsel), sta0 = mbits_of(hsta), stn0 = mbits_of(hstn);
 
-  // cooperative stores of the dirty granules: every LDS read first (one wait), then the stores
-  {
-    constexpr int KA = n_items<kPvG>(), KB = n_items<6>(), KC = n_items<3>();
-    uint4 va[KA], vb[KB], vc[KC], vd[KD], ve[KE];
-    uint32_t pa[KA], pc[KC], pd[KD], pe[KE], wd[KD], we[KE];
+  bool finish = false;
+  const bool was_done = R.done() != 0u;
+  if (!was_done) finish = step_regs(R, act, s, i, na);
+  if (finish) R.set_done(1u);
+
+  // store back what changed
+  uint4 *pw = reinterpret_cast<uint4 *>(s.priv + i);
+  const uint4 g0n = make_uint4(R.rng, R.seed, R.max_steps, R.turn_counter);
+  const uint4 g1n = make_uint4(R.g1x, R.g1y, R.in_market, R.flags);
+  if (ne4(g0n, g0)) pw[0] = g0n;
+  if (ne4(g1n, g1)) pw[1] = g1n;
+  if (R.moved) pw[2] = R.g2;
+  if (R.info_steps != info_steps) reinterpret_cast<uint32_t *>(pw + 3)[0] = R.info_steps;
+  const uint4 plan = pack_player(R.P);
+  if (ne4(plan, pla)) pw[4 + ag] = plan;
+  if (R.moved) reinterpret_cast<uint2 *>(pw + 8)[ag] = R.cells_a;
+  const uint4 shn[3] = {make_uint4(R.sh[0], R.sh[1], R.sh[2], R.sh[3]), make_uint4(R.sh[4], R.sh[5], R.sh[6], R.sh[7]),
+                        make_uint4(R.sh[8], R.sh[9], R.sh[10], R.sh[11])};
 #pragma unroll
-    for (int k = 0; k < KA; k++) {
-      const int e = item_env<kPvG>(k, lane), g = item_gran<kPvG>(k, lane);
-      pa[k] = (slot_of(e)[SLOT_PLAN / 4] >> g) & 1u;
-      va[k] = lds_get4(slot_of(e) + SLOT_PV / 4 + 4 * g);
-    }
+  for (int k = 0; k < 3; k++)
+    if (ne4(shn[k], sh_in[k])) reinterpret_cast<uint4 *>(ob + COG_OBS_PHASE)[k] = shn[k];
 #pragma unroll
-    for (int k = 0; k < KB; k++) {
-      const int e = item_env<6>(k, lane), g = item_gran<6>(k, lane);
-      vb[k] = lds_get4(slot_of(e) + SLOT_SEL / 4 + 4 * g);
-    }
-#pragma unroll
-    for (int k = 0; k < KC; k++) {
-      const int e = item_env<3>(k, lane), g = item_gran<3>(k, lane);
-      pc[k] = (slot_of(e)[SLOT_PLAN / 4] >> (10 + g)) & 1u;
-      vc[k] = lds_get4(slot_of(e) + SLOT_SH / 4 + 4 * g);
-    }
-#pragma unroll
-    for (int k = 0; k < KD; k++) {                         // deck granules = plan bits 13..19,
-      const int e = item_env<13>(k, lane), g = item_gran<13>(k, lane);   // stored mask = bits 20..25
-      pd[k] = (slot_of(e)[SLOT_PLAN / 4] >> (13 + g)) & 1u;
-      wd[k] = slot_of(e)[SLOT_PLAN / 4 + 1] & 3u;
-      vd[k] = lds_get4(slot_of(e) + SLOT_DK / 4 + 4 * g);
-    }
-#pragma unroll
-    for (int k = 0; k < KE; k++) {                         // na's stored mask = bits 26..31
-      const int e = item_env<6>(k, lane), g = item_gran<6>(k, lane);
-      pe[k] = (slot_of(e)[SLOT_PLAN / 4] >> (26 + g)) & 1u;
-      we[k] = (slot_of(e)[SLOT_PLAN / 4 + 1] >> 2) & 3u;
-      ve[k] = lds_get4(slot_of(e) + SLOT_STN / 4 + 4 * g);
-    }
-#pragma unroll
-    for (int k = 0; k < KA; k++) {
-      const int e = item_env<kPvG>(k, lane), g = item_gran<kPvG>(k, lane);
-      if (pa[k]) reinterpret_cast<uint4 *>(s.priv + base + e)[g] = va[k];
-    }
-#pragma unroll
-    for (int k = 0; k < KB; k++) {
-      const int e = item_env<6>(k, lane), g = item_gran<6>(k, lane);
-      if (e < nv) reinterpret_cast<uint4 *>(s.sel + (base + e) * COG_MASK_BYTES)[g] = vb[k];
-    }
-#pragma unroll
-    for (int k = 0; k < KC; k++) {
-      const int e = item_env<3>(k, lane), g = item_gran<3>(k, lane);
-      if (pc[k]) reinterpret_cast<uint4 *>(obs_of(e) + COG_OBS_PHASE)[g] = vc[k];
-    }
-#pragma unroll
-    for (int k = 0; k < KD; k++) {
-      const int e = item_env<13>(k, lane), g = item_gran<13>(k, lane);
-      if (pd[k]) reinterpret_cast<uint4 *>(player_of(e, wd[k]))[g < 7 ? g : g + 1] = vd[k];
-    }
-#pragma unroll
-    for (int k = 0; k < KE; k++) {
-      const int e = item_env<6>(k, lane), g = item_gran<6>(k, lane);
-      if (pe[k]) reinterpret_cast<uint4 *>(player_of(e, we[k]) + COG_PD_MASK)[g] = ve[k];
-    }
+  for (int k = 0; k < 7; k++) {
+    const uint4 v = make_uint4(R.d[4 * k], R.d[4 * k + 1], R.d[4 * k + 2], R.d[4 * k + 3]);
+    if (ne4(v, dk[k])) reinterpret_cast<uint4 *>(deck)[k] = v;
   }
-  STAMP(s, 12);
-  wave_encode(s, base + lane, enc);
+  {
+    const MBits b = bits_of(R.sel);
+    const uint32_t gm = mask_diff_granules(b, sel0);
+    if (gm) s.heads[5 * i] = mbits_u4(b);
+    uint4 *rec = reinterpret_cast<uint4 *>(s.sel + i * COG_MASK_BYTES);
+#pragma unroll
+    for (int g = 0; g < 6; g++)
+      if ((gm >> g) & 1u) rec[g] = mask_granule(b, g);
+  }
+  {
+    const MBits b = bits_of(R.sta);
+    const uint32_t gm = mask_diff_granules(b, sta0);
+    if (gm) s.heads[5 * i + 1 + ag] = mbits_u4(b);
+    uint4 *rec = reinterpret_cast<uint4 *>(deck + COG_PD_MASK);
+#pragma unroll
+    for (int g = 0; g < 6; g++)
+      if ((gm >> g) & 1u) rec[g] = mask_granule(b, g);
+  }
+  if (na != ag) {
+    const MBits b = bits_of(R.stn);
+    const uint32_t gm = mask_diff_granules(b, stn0);
+    if (gm) s.heads[5 * i + 1 + na] = mbits_u4(b);
+    uint4 *rec = reinterpret_cast<uint4 *>(ob + COG_OBS_PLAYER0 + COG_OBS_PLAYER_STRIDE * na + COG_PD_MASK);
+#pragma unroll
+    for (int g = 0; g < 6; g++)
+      if ((gm >> g) & 1u) rec[g] = mask_granule(b, g);
+  }
+
+  // episode end / auto-reset: rare, on the stored state (vec_environment.h:56-59)
+  if (finish) finish_episode(make_ctx(s, i));
+  const bool done = was_done || finish;
+  s.done[i] = done ? 1 : 0;                                // dones[i] before the auto-reset
+  bool enc = false;
+  uint32_t agent = R.agent();
+  if (done) {
+    Ctx e = make_ctx(s, i);
+    if (!env_reset(e)) {
+      atomicOr(&s.status[0], e.pv->flags);
+      atomicAdd(&s.status[1], 1u);
+    } else {
+      enc = true;
+      const uint32_t k = atomicAdd(&s.status[2], 1u);
+      if (k < s.n) s.dirty[k] = (uint32_t)i;
+    }
+    sync_heads(s, i);
+    agent = e.pv->agent;
+  }
+  s.agent[i] = (uint8_t)agent;
+  return enc;
 }
 
-__global__ void __launch_bounds__(64) k_step(DevState s, const uint8_t *__restrict__ actions) {
-  __shared__ uint32_t slots[kWaveEnvs * kSlotWords];
-  wave_step(s, slots, actions, 0, nullptr, nullptr);
+template <int SRC>
+__global__ void __launch_bounds__(64) k_env_step(DevState s, const uint8_t *__restrict__ act_in, uint32_t *__restrict__ rngs,
+                                                 uint8_t *__restrict__ actions_out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool enc = false;
+  if (i < s.n) enc = env_step_lane<SRC>(s, i, act_in, rngs, actions_out);
+  wave_encode(s, i < s.n ? i : 0, enc);                    // converged: the whole wave encodes
 }
 
 __global__ void __launch_bounds__(256) k_sample(size_t n, const uint8_t *__restrict__ masks,
@@ -1530,10 +1530,9 @@ __global__ void __launch_bounds__(256) k_sample(size_t n, const uint8_t *__restr
   store_action(actions + i * COG_ACTION_BYTES, a);
 }
 
-__global__ void __launch_bounds__(64) k_sample_step(DevState s, int mask_source, uint32_t *__restrict__ rngs,
-                                                    uint8_t *__restrict__ actions) {
-  __shared__ uint32_t slots[kWaveEnvs * kSlotWords];
-  wave_step(s, slots, nullptr, mask_source, rngs, actions);
+__global__ void k_sync_heads(DevState s) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < s.n) sync_heads(s, i);
 }
 
 __global__ void k_seed_sampler(size_t n, uint32_t seed, uint32_t *rngs) {
@@ -1549,11 +1548,13 @@ static inline unsigned blocks_for(size_t n, unsigned t) { return (unsigned)((n +
 int launch_init(const DevState &s, const uint32_t *, uint32_t default_seed, void *stream) {
   if (!s.n) return 0;
   hipLaunchKernelGGL(k_init, dim3(blocks_for(s.n, 256)), dim3(256), 0, (hipStream_t)stream, s, default_seed);
+  hipLaunchKernelGGL(k_sync_heads, dim3(blocks_for(s.n, 256)), dim3(256), 0, (hipStream_t)stream, s);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_reset(const DevState &s, const ResetParams &p, void *stream) {
   if (!s.n) return 0;
   hipLaunchKernelGGL(k_reset, dim3(blocks_for(s.n, 64)), dim3(64), 0, (hipStream_t)stream, s, p);
+  hipLaunchKernelGGL(k_sync_heads, dim3(blocks_for(s.n, 256)), dim3(256), 0, (hipStream_t)stream, s);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_encode_all(const DevState &s, void *stream, int variant) {
@@ -1569,7 +1570,8 @@ int launch_encode_all(const DevState &s, void *stream, int variant) {
 }
 int launch_step(const DevState &s, const uint8_t *d_actions, void *stream) {
   if (!s.n) return 0;
-  hipLaunchKernelGGL(k_step, dim3(blocks_for(s.n, kWaveEnvs)), dim3(kWaveEnvs), 0, (hipStream_t)stream, s, d_actions);
+  hipLaunchKernelGGL(k_env_step<MASK_EXTERNAL>, dim3(blocks_for(s.n, 64)), dim3(64), 0, (hipStream_t)stream, s,
+                     d_actions, nullptr, nullptr);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_sample(size_t n, const uint8_t *d_masks, uint32_t *d_rng, uint8_t *d_actions, void *stream) {
@@ -1579,8 +1581,12 @@ int launch_sample(size_t n, const uint8_t *d_masks, uint32_t *d_rng, uint8_t *d_
 }
 int launch_sample_step(const DevState &s, int mask_source, uint32_t *d_rng, uint8_t *d_actions, void *stream) {
   if (!s.n) return 0;
-  hipLaunchKernelGGL(k_sample_step, dim3(blocks_for(s.n, kWaveEnvs)), dim3(kWaveEnvs), 0, (hipStream_t)stream, s,
-                     mask_source, d_rng, d_actions);
+  if (mask_source == MASK_STORED)
+    hipLaunchKernelGGL(k_env_step<MASK_STORED>, dim3(blocks_for(s.n, 64)), dim3(64), 0, (hipStream_t)stream, s,
+                       nullptr, d_rng, d_actions);
+  else
+    hipLaunchKernelGGL(k_env_step<MASK_SELECTED>, dim3(blocks_for(s.n, 64)), dim3(64), 0, (hipStream_t)stream, s,
+                       nullptr, d_rng, d_actions);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_seed_sampler(size_t n, uint32_t seed, uint32_t *d_rng, void *stream) {
