@@ -95,7 +95,9 @@ struct DevState {
   uint4 *heads;                      // [n][5] mask bit-vectors: selected, stored of players 0..3
   GenScratch *gen;
   uint32_t *status;                  // [0] OR of error flags, [1] error count, [2] dirty count
-  uint32_t *dirty;                   // [n] envs whose map was re-generated (host view refresh)
+  uint32_t *dirty;                   // [cap] envs whose map was re-generated (host view refresh)
+  size_t first;                      // global index of env 0 (sub-range launches; dirty list ids)
+  size_t cap;                        // capacity of the dirty list
   unsigned long long *stamps;        // diagnostic builds (COG_STAMPS) only: per-wave phase clocks
 };
 
@@ -104,6 +106,25 @@ struct ResetParams {
   uint8_t n_players, n_pieces, difficulty, use_params;   // use_params=0: cog_env::reset()
   uint32_t max_steps;
 };
+
+// the envs [lo, hi) of s as a state of their own (per-stream sub-range launches)
+inline DevState sub_state(const DevState &s, size_t lo, size_t hi) {
+  DevState t = s;
+  t.n = hi - lo;
+  t.first = s.first + lo;
+  t.obs += lo * COG_OBS_BYTES;
+  t.sel += lo * COG_MASK_BYTES;
+  t.info += lo * COG_INFO_BYTES;
+  t.rew += lo * 4;
+  t.done += lo;
+  t.agent += lo;
+  t.priv += lo;
+  t.grid += lo * (size_t)kGridBytes;
+  t.cgrid += lo * (size_t)COG_CELLS;
+  t.heads += lo * 5;
+  t.gen += lo;
+  return t;
+}
 
 enum MaskSource : int { MASK_SELECTED = 0, MASK_STORED = 1, MASK_EXTERNAL = 2 };
 
@@ -117,6 +138,9 @@ int launch_sample(size_t n, const uint8_t *d_masks, uint32_t *d_rng, uint8_t *d_
                   void *stream);
 int launch_sample_step(const DevState &s, int mask_source, uint32_t *d_rng, uint8_t *d_actions,
                        void *stream);
+int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions,
+                   void *stream);                    // persistent K-step runner loop
 int launch_seed_sampler(size_t n, uint32_t seed, uint32_t *d_rng, void *stream);
+int launch_spin(uint32_t ns, void *stream);         // a one-wave kernel that waits ~ns (stream stagger)
 
 }  // namespace cog

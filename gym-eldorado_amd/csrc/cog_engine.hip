@@ -1367,48 +1367,117 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
   return COG_HEX_END(c0) || R.turn_counter >= R.max_steps;
 }
 
-// One env per work-item: load (two rounds), [sample], step, store what changed, [auto-reset].
-// SRC: MASK_SELECTED / MASK_STORED (runner, sampling fused) or MASK_EXTERNAL (host actions).
-template <int SRC>
-DEV bool env_step_lane(const DevState &s, size_t i, const uint8_t *act_in, uint32_t *rngs, uint8_t *actions_out) {
-  RegEnv R;
+// ---- lane drivers ---------------------------------------------------------------------------
+// Snap: the step-start image of everything a step may modify; the store phase writes back the
+// 16-B granules that differ from it (and nothing else).
+struct Snap {
+  uint4 g0, g1;                       // EnvPriv granules 0, 1
+  uint32_t info_steps;                // EnvPriv granule 3, dword 0
+  uint4 sh[3];                        // ObsData 16128..16175: phase, resources, shop
+  MBits sel;                          // selected mask
+  uint4 pla, pln;                     // pl[ag], pl[na]
+  uint2 ca, cn;                       // cells[ag], cells[na]
+  MBits sta, stn;                     // stored masks of ag, na
+  uint4 dk[7];                        // DeckObs of ag
+};
+
+DEV void load_env(const DevState &s, size_t i, Snap &S) {          // records at fixed addresses
   const uint4 *pv4 = reinterpret_cast<const uint4 *>(s.priv + i);
-  uint8_t *ob = s.obs + i * COG_OBS_BYTES;
-  // round 1: records at fixed addresses
-  const uint4 g0 = pv4[0], g1 = pv4[1];
-  const uint32_t info_steps = reinterpret_cast<const uint32_t *>(pv4 + 3)[0];
-  const uint4 hsel = s.heads[5 * i];
-  const uint4 sh0 = reinterpret_cast<const uint4 *>(ob + COG_OBS_PHASE)[0];
-  const uint4 sh1 = reinterpret_cast<const uint4 *>(ob + COG_OBS_PHASE)[1];
-  const uint4 sh2 = reinterpret_cast<const uint4 *>(ob + COG_OBS_PHASE)[2];
-  uint32_t srng = SRC == MASK_EXTERNAL ? 0u : rngs[i];
-  R.rng = g0.x; R.seed = g0.y; R.max_steps = g0.z; R.turn_counter = g0.w;
-  R.g1x = g1.x; R.g1y = g1.y; R.in_market = g1.z; R.flags = g1.w;
-  R.info_steps = info_steps;
-  R.moved = false;
-  const int ag = (int)R.agent();
-  const int na = ag + 1 >= (int)R.n_players() ? 0 : ag + 1;
-  // round 2: the acting / next player's records
-  const uint4 pla = pv4[4 + ag], pln = pv4[4 + na];
-  R.cells_a = reinterpret_cast<const uint2 *>(pv4 + 8)[ag];
-  R.cells_n = reinterpret_cast<const uint2 *>(pv4 + 8)[na];
-  const uint4 hsta = s.heads[5 * i + 1 + ag], hstn = s.heads[5 * i + 1 + na];
-  uint8_t *deck = ob + COG_OBS_PLAYER0 + COG_OBS_PLAYER_STRIDE * ag;
-  uint4 dk[7];
+  const uint4 *sh4 = reinterpret_cast<const uint4 *>(s.obs + i * COG_OBS_BYTES + COG_OBS_PHASE);
+  S.g0 = pv4[0];
+  S.g1 = pv4[1];
+  S.info_steps = reinterpret_cast<const uint32_t *>(pv4 + 3)[0];
+  S.sel = mbits_of(s.heads[5 * i]);
+  S.sh[0] = sh4[0];
+  S.sh[1] = sh4[1];
+  S.sh[2] = sh4[2];
+}
+DEV uint8_t *deck_ptr(const DevState &s, size_t i, int p) {
+  return s.obs + i * COG_OBS_BYTES + COG_OBS_PLAYER0 + COG_OBS_PLAYER_STRIDE * p;
+}
+DEV void load_players(const DevState &s, size_t i, int ag, int na, Snap &S) {   // acting / next
+  const uint4 *pv4 = reinterpret_cast<const uint4 *>(s.priv + i);
+  S.pla = pv4[4 + ag];
+  S.pln = pv4[4 + na];
+  S.ca = reinterpret_cast<const uint2 *>(pv4 + 8)[ag];
+  S.cn = reinterpret_cast<const uint2 *>(pv4 + 8)[na];
+  S.sta = mbits_of(s.heads[5 * i + 1 + ag]);
+  S.stn = mbits_of(s.heads[5 * i + 1 + na]);
+  const uint4 *dk = reinterpret_cast<const uint4 *>(deck_ptr(s, i, ag));
 #pragma unroll
-  for (int k = 0; k < 7; k++) dk[k] = reinterpret_cast<const uint4 *>(deck)[k];
-  // the sampler needs round 1 only: it runs while round 2 is in flight
-  R.sel = heads_of(mbits_of(hsel));
-  uint8_t act[5];
+  for (int k = 0; k < 7; k++) S.dk[k] = dk[k];
+}
+DEV void regs_env(RegEnv &R, const Snap &S) {
+  R.rng = S.g0.x; R.seed = S.g0.y; R.max_steps = S.g0.z; R.turn_counter = S.g0.w;
+  R.g1x = S.g1.x; R.g1y = S.g1.y; R.in_market = S.g1.z; R.flags = S.g1.w;
+  R.info_steps = S.info_steps;
+  R.moved = false;
+  R.sel = heads_of(S.sel);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    R.sh[4 * k] = S.sh[k].x; R.sh[4 * k + 1] = S.sh[k].y; R.sh[4 * k + 2] = S.sh[k].z; R.sh[4 * k + 3] = S.sh[k].w;
+  }
+}
+DEV void regs_players(RegEnv &R, const Snap &S) {
+  R.P = unpack_player(S.pla);
+  R.na_active = (S.pln.y >> 16) & 0xffu;
+  R.cells_a = S.ca;
+  R.cells_n = S.cn;
+  R.sta = heads_of(S.sta);
+  R.stn = heads_of(S.stn);
+#pragma unroll
+  for (int k = 0; k < 7; k++) {
+    R.d[4 * k] = S.dk[k].x; R.d[4 * k + 1] = S.dk[k].y; R.d[4 * k + 2] = S.dk[k].z; R.d[4 * k + 3] = S.dk[k].w;
+  }
+}
+DEV void store_mask_record(uint4 *rec, const MBits &b, uint32_t gm) {
+#pragma unroll
+  for (int g = 0; g < 6; g++)
+    if ((gm >> g) & 1u) rec[g] = mask_granule(b, g);
+}
+// write back every granule that differs from the step-start image S (ag / na: players of S)
+DEV void store_changes(const DevState &s, size_t i, int ag, int na, const Snap &S, const RegEnv &R) {
+  uint4 *pw = reinterpret_cast<uint4 *>(s.priv + i);
+  uint8_t *ob = s.obs + i * COG_OBS_BYTES;
+  const uint4 g0n = make_uint4(R.rng, R.seed, R.max_steps, R.turn_counter);
+  const uint4 g1n = make_uint4(R.g1x, R.g1y, R.in_market, R.flags);
+  if (ne4(g0n, S.g0)) pw[0] = g0n;
+  if (ne4(g1n, S.g1)) pw[1] = g1n;
+  if (R.moved) pw[2] = R.g2;
+  if (R.info_steps != S.info_steps) reinterpret_cast<uint32_t *>(pw + 3)[0] = R.info_steps;
+  const uint4 pl = pack_player(R.P);
+  if (ne4(pl, S.pla)) pw[4 + ag] = pl;
+  if (R.moved) reinterpret_cast<uint2 *>(pw + 8)[ag] = R.cells_a;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const uint4 v = make_uint4(R.sh[4 * k], R.sh[4 * k + 1], R.sh[4 * k + 2], R.sh[4 * k + 3]);
+    if (ne4(v, S.sh[k])) reinterpret_cast<uint4 *>(ob + COG_OBS_PHASE)[k] = v;
+  }
+  uint8_t *deck = deck_ptr(s, i, ag);
+#pragma unroll
+  for (int k = 0; k < 7; k++) {
+    const uint4 v = make_uint4(R.d[4 * k], R.d[4 * k + 1], R.d[4 * k + 2], R.d[4 * k + 3]);
+    if (ne4(v, S.dk[k])) reinterpret_cast<uint4 *>(deck)[k] = v;
+  }
+  const MBits bs = bits_of(R.sel), ba = bits_of(R.sta), bn = bits_of(R.stn);
+  const uint32_t gs = mask_diff_granules(bs, S.sel), ga = mask_diff_granules(ba, S.sta),
+                 gn = na != ag ? mask_diff_granules(bn, S.stn) : 0u;
+  if (gs) s.heads[5 * i] = mbits_u4(bs);
+  if (ga) s.heads[5 * i + 1 + ag] = mbits_u4(ba);
+  if (gn) s.heads[5 * i + 1 + na] = mbits_u4(bn);
+  store_mask_record(reinterpret_cast<uint4 *>(s.sel + i * COG_MASK_BYTES), bs, gs);
+  store_mask_record(reinterpret_cast<uint4 *>(deck + COG_PD_MASK), ba, ga);
+  store_mask_record(reinterpret_cast<uint4 *>(deck_ptr(s, i, na) + COG_PD_MASK), bn, gn);
+}
+
+// the action of this step: sampled (runner) or the host's (indices past a head are the
+// reference's out-of-range accesses: clamped and flagged)
+template <int SRC>
+DEV void step_action(RegEnv &R, const uint8_t *act_in, size_t i, uint32_t &srng, uint8_t act[5]) {
   if (SRC == MASK_SELECTED) sample_heads(R.sel, srng, act);
-  // unpack round 2
-  R.P = unpack_player(pla);
-  R.na_active = (pln.y >> 16) & 0xffu;
-  R.sta = heads_of(mbits_of(hsta));
-  R.stn = heads_of(mbits_of(hstn));
-  if (SRC == MASK_STORED) sample_heads(R.sta, srng, act);
-  if (SRC == MASK_EXTERNAL) {                              // host actions: indices past a head
-    const uint8_t *ai = act_in + i * COG_ACTION_BYTES;     // are the reference's OOB accesses
+  else if (SRC == MASK_STORED) sample_heads(R.sta, srng, act);
+  else {
+    const uint8_t *ai = act_in + i * COG_ACTION_BYTES;
     const uint8_t top[5] = {COG_N_CARDTYPES, COG_N_CARDTYPES, COG_N_CARDTYPES, 6, COG_N_SHOP};
 #pragma unroll
     for (int k = 0; k < 5; k++) {
@@ -1418,81 +1487,16 @@ DEV bool env_step_lane(const DevState &s, size_t i, const uint8_t *act_in, uint3
         R.flags |= F_BAD_ACTION;
       }
     }
-  } else {
-    rngs[i] = srng;
-    store_action(actions_out + i * COG_ACTION_BYTES, act);
   }
-  const uint4 sh_in[3] = {sh0, sh1, sh2};
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    R.sh[4 * k] = sh_in[k].x; R.sh[4 * k + 1] = sh_in[k].y; R.sh[4 * k + 2] = sh_in[k].z; R.sh[4 * k + 3] = sh_in[k].w;
-  }
-#pragma unroll
-  for (int k = 0; k < 7; k++) {
-    R.d[4 * k] = dk[k].x; R.d[4 * k + 1] = dk[k].y; R.d[4 * k + 2] = dk[k].z; R.d[4 * k + 3] = dk[k].w;
-  }
-  const MBits sel0 = mbits_of(hsel), sta0 = mbits_of(hsta), stn0 = mbits_of(hstn);
+}
 
-  bool finish = false;
-  const bool was_done = R.done() != 0u;
-  if (!was_done) finish = step_regs(R, act, s, i, na);
-  if (finish) R.set_done(1u);
-
-  // store back what changed
-  uint4 *pw = reinterpret_cast<uint4 *>(s.priv + i);
-  const uint4 g0n = make_uint4(R.rng, R.seed, R.max_steps, R.turn_counter);
-  const uint4 g1n = make_uint4(R.g1x, R.g1y, R.in_market, R.flags);
-  if (ne4(g0n, g0)) pw[0] = g0n;
-  if (ne4(g1n, g1)) pw[1] = g1n;
-  if (R.moved) pw[2] = R.g2;
-  if (R.info_steps != info_steps) reinterpret_cast<uint32_t *>(pw + 3)[0] = R.info_steps;
-  const uint4 plan = pack_player(R.P);
-  if (ne4(plan, pla)) pw[4 + ag] = plan;
-  if (R.moved) reinterpret_cast<uint2 *>(pw + 8)[ag] = R.cells_a;
-  const uint4 shn[3] = {make_uint4(R.sh[0], R.sh[1], R.sh[2], R.sh[3]), make_uint4(R.sh[4], R.sh[5], R.sh[6], R.sh[7]),
-                        make_uint4(R.sh[8], R.sh[9], R.sh[10], R.sh[11])};
-#pragma unroll
-  for (int k = 0; k < 3; k++)
-    if (ne4(shn[k], sh_in[k])) reinterpret_cast<uint4 *>(ob + COG_OBS_PHASE)[k] = shn[k];
-#pragma unroll
-  for (int k = 0; k < 7; k++) {
-    const uint4 v = make_uint4(R.d[4 * k], R.d[4 * k + 1], R.d[4 * k + 2], R.d[4 * k + 3]);
-    if (ne4(v, dk[k])) reinterpret_cast<uint4 *>(deck)[k] = v;
-  }
-  {
-    const MBits b = bits_of(R.sel);
-    const uint32_t gm = mask_diff_granules(b, sel0);
-    if (gm) s.heads[5 * i] = mbits_u4(b);
-    uint4 *rec = reinterpret_cast<uint4 *>(s.sel + i * COG_MASK_BYTES);
-#pragma unroll
-    for (int g = 0; g < 6; g++)
-      if ((gm >> g) & 1u) rec[g] = mask_granule(b, g);
-  }
-  {
-    const MBits b = bits_of(R.sta);
-    const uint32_t gm = mask_diff_granules(b, sta0);
-    if (gm) s.heads[5 * i + 1 + ag] = mbits_u4(b);
-    uint4 *rec = reinterpret_cast<uint4 *>(deck + COG_PD_MASK);
-#pragma unroll
-    for (int g = 0; g < 6; g++)
-      if ((gm >> g) & 1u) rec[g] = mask_granule(b, g);
-  }
-  if (na != ag) {
-    const MBits b = bits_of(R.stn);
-    const uint32_t gm = mask_diff_granules(b, stn0);
-    if (gm) s.heads[5 * i + 1 + na] = mbits_u4(b);
-    uint4 *rec = reinterpret_cast<uint4 *>(ob + COG_OBS_PLAYER0 + COG_OBS_PLAYER_STRIDE * na + COG_PD_MASK);
-#pragma unroll
-    for (int g = 0; g < 6; g++)
-      if ((gm >> g) & 1u) rec[g] = mask_granule(b, g);
-  }
-
-  // episode end / auto-reset: rare, on the stored state (vec_environment.h:56-59)
+// episode end + dones[i] + auto-reset (environment.cpp:187-207, vec_environment.h:56-59) on the
+// stored state; returns true when the env's map was regenerated (the wave encodes it)
+DEV bool end_of_step(const DevState &s, size_t i, bool was_done, bool finish, uint32_t &agent) {
   if (finish) finish_episode(make_ctx(s, i));
   const bool done = was_done || finish;
   s.done[i] = done ? 1 : 0;                                // dones[i] before the auto-reset
   bool enc = false;
-  uint32_t agent = R.agent();
   if (done) {
     Ctx e = make_ctx(s, i);
     if (!env_reset(e)) {
@@ -1501,12 +1505,46 @@ DEV bool env_step_lane(const DevState &s, size_t i, const uint8_t *act_in, uint3
     } else {
       enc = true;
       const uint32_t k = atomicAdd(&s.status[2], 1u);
-      if (k < s.n) s.dirty[k] = (uint32_t)i;
+      if (k < s.cap) s.dirty[k] = (uint32_t)(s.first + i);
     }
     sync_heads(s, i);
     agent = e.pv->agent;
   }
   s.agent[i] = (uint8_t)agent;
+  return enc;
+}
+
+// One step of env i: load (two rounds; the sampler runs on round 1 while round 2 is in
+// flight), step on registers, store what changed, [finish / auto-reset].
+template <int SRC>
+DEV bool env_step_lane(const DevState &s, size_t i, const uint8_t *act_in, uint32_t *rngs, uint8_t *actions_out) {
+  STAMP(s, 0);
+  Snap S;
+  RegEnv R;
+  load_env(s, i, S);
+  uint32_t srng = SRC == MASK_EXTERNAL ? 0u : rngs[i];
+  regs_env(R, S);
+  const int ag = (int)R.agent();
+  const int na = ag + 1 >= (int)R.n_players() ? 0 : ag + 1;
+  load_players(s, i, ag, na, S);
+  uint8_t act[5];
+  if (SRC == MASK_SELECTED) step_action<SRC>(R, act_in, i, srng, act);
+  regs_players(R, S);
+  if (SRC != MASK_SELECTED) step_action<SRC>(R, act_in, i, srng, act);
+  if (SRC != MASK_EXTERNAL) {
+    rngs[i] = srng;
+    store_action(actions_out + i * COG_ACTION_BYTES, act);
+  }
+  STAMP(s, 1);
+  const bool was_done = R.done() != 0u;
+  const bool finish = !was_done && step_regs(R, act, s, i, na);
+  if (finish) R.set_done(1u);
+  STAMP(s, 2);
+  store_changes(s, i, ag, na, S, R);
+  STAMP(s, 3);
+  uint32_t agent = R.agent();
+  const bool enc = end_of_step(s, i, was_done, finish, agent);
+  STAMP(s, 4);
   return enc;
 }
 
@@ -1517,6 +1555,98 @@ __global__ void __launch_bounds__(64) k_env_step(DevState s, const uint8_t *__re
   bool enc = false;
   if (i < s.n) enc = env_step_lane<SRC>(s, i, act_in, rngs, actions_out);
   wave_encode(s, i < s.n ? i : 0, enc);                    // converged: the whole wave encodes
+  STAMP(s, 5);
+}
+
+// Persistent rollout: K x (sample; step) per launch (the runner's device loop, runner.h:46-55).
+// Every step stores its outputs exactly as a single-step launch does (the HBM state after each
+// step is the reference's); what changes is where the next step reads its inputs from: the
+// env-level records stay in VGPRs and every player's records (deck, counters, neighbourhood
+// cache, stored mask) in this wave's LDS, so a step issues no global loads unless it resets.
+struct LaneLds {
+  uint4 deck[4][7][64];               // [player][granule][lane]: lane-contiguous, conflict-free
+  uint4 pl[4][64];
+  uint2 cells[4][64];
+  uint4 heads[4][64];                 // stored masks (MBits + pad)
+};
+DEV void lds_fill_players(LaneLds &L, const DevState &s, size_t i, int l) {
+  const uint4 *pv4 = reinterpret_cast<const uint4 *>(s.priv + i);
+#pragma unroll
+  for (int p = 0; p < 4; p++) {
+    const uint4 *dk = reinterpret_cast<const uint4 *>(deck_ptr(s, i, p));
+#pragma unroll
+    for (int k = 0; k < 7; k++) L.deck[p][k][l] = dk[k];
+    L.pl[p][l] = pv4[4 + p];
+    L.cells[p][l] = reinterpret_cast<const uint2 *>(pv4 + 8)[p];
+    L.heads[p][l] = s.heads[5 * i + 1 + p];
+  }
+}
+DEV void lds_players(const LaneLds &L, int l, int ag, int na, Snap &S) {
+  S.pla = L.pl[ag][l];
+  S.pln = L.pl[na][l];
+  S.ca = L.cells[ag][l];
+  S.cn = L.cells[na][l];
+  S.sta = mbits_of(L.heads[ag][l]);
+  S.stn = mbits_of(L.heads[na][l]);
+#pragma unroll
+  for (int k = 0; k < 7; k++) S.dk[k] = L.deck[ag][k][l];
+}
+
+template <int SRC>
+__global__ void __launch_bounds__(64) k_env_rollout(DevState s, int steps, uint32_t *__restrict__ rngs,
+                                                    uint8_t *__restrict__ actions_out) {
+  __shared__ LaneLds L;
+  const int l = threadIdx.x;
+  const size_t i0 = (size_t)blockIdx.x * blockDim.x + l;
+  const bool live = i0 < s.n;
+  const size_t i = live ? i0 : 0;
+  Snap S;
+  uint32_t srng = 0;
+  if (live) {
+    load_env(s, i, S);
+    lds_fill_players(L, s, i, l);
+    srng = rngs[i];
+  }
+  for (int t = 0; t < steps; t++) {
+    bool enc = false;
+    if (live) {
+      RegEnv R;
+      regs_env(R, S);
+      const int ag = (int)R.agent();
+      const int na = ag + 1 >= (int)R.n_players() ? 0 : ag + 1;
+      lds_players(L, l, ag, na, S);
+      uint8_t act[5];
+      if (SRC == MASK_SELECTED) step_action<SRC>(R, nullptr, i, srng, act);
+      regs_players(R, S);
+      if (SRC == MASK_STORED) step_action<SRC>(R, nullptr, i, srng, act);
+      rngs[i] = srng;
+      store_action(actions_out + i * COG_ACTION_BYTES, act);
+      const bool was_done = R.done() != 0u;
+      const bool finish = !was_done && step_regs(R, act, s, i, na);
+      if (finish) R.set_done(1u);
+      store_changes(s, i, ag, na, S, R);
+      // the next step's image: registers (env level) and this wave's LDS (player level)
+      S.g0 = make_uint4(R.rng, R.seed, R.max_steps, R.turn_counter);
+      S.g1 = make_uint4(R.g1x, R.g1y, R.in_market, R.flags);
+      S.info_steps = R.info_steps;
+#pragma unroll
+      for (int k = 0; k < 3; k++) S.sh[k] = make_uint4(R.sh[4 * k], R.sh[4 * k + 1], R.sh[4 * k + 2], R.sh[4 * k + 3]);
+      S.sel = bits_of(R.sel);
+      L.pl[ag][l] = pack_player(R.P);
+      L.cells[ag][l] = R.cells_a;
+      L.heads[ag][l] = mbits_u4(bits_of(R.sta));
+      if (na != ag) L.heads[na][l] = mbits_u4(bits_of(R.stn));
+#pragma unroll
+      for (int k = 0; k < 7; k++) L.deck[ag][k][l] = make_uint4(R.d[4 * k], R.d[4 * k + 1], R.d[4 * k + 2], R.d[4 * k + 3]);
+      uint32_t agent = R.agent();
+      enc = end_of_step(s, i, was_done, finish, agent);
+      if (was_done || finish) {                            // reset: reload from the stored state
+        load_env(s, i, S);
+        lds_fill_players(L, s, i, l);
+      }
+    }
+    wave_encode(s, i, enc);                                // converged: the whole wave encodes
+  }
 }
 
 __global__ void __launch_bounds__(256) k_sample(size_t n, const uint8_t *__restrict__ masks,
@@ -1533,6 +1663,11 @@ __global__ void __launch_bounds__(256) k_sample(size_t n, const uint8_t *__restr
 __global__ void k_sync_heads(DevState s) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < s.n) sync_heads(s, i);
+}
+
+__global__ void k_spin(uint32_t ns) {                      // wall clock: 100 MHz s_memrealtime
+  const uint64_t t0 = wall_clock64(), ticks = ns / 10u;
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
 }
 
 __global__ void k_seed_sampler(size_t n, uint32_t seed, uint32_t *rngs) {
@@ -1587,6 +1722,20 @@ int launch_sample_step(const DevState &s, int mask_source, uint32_t *d_rng, uint
   else
     hipLaunchKernelGGL(k_env_step<MASK_SELECTED>, dim3(blocks_for(s.n, 64)), dim3(64), 0, (hipStream_t)stream, s,
                        nullptr, d_rng, d_actions);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int launch_spin(uint32_t ns, void *stream) {
+  hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, (hipStream_t)stream, ns);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions, void *stream) {
+  if (!s.n || steps <= 0) return 0;
+  if (mask_source == MASK_STORED)
+    hipLaunchKernelGGL(k_env_rollout<MASK_STORED>, dim3(blocks_for(s.n, 64)), dim3(64), 0, (hipStream_t)stream, s,
+                       steps, d_rng, d_actions);
+  else
+    hipLaunchKernelGGL(k_env_rollout<MASK_SELECTED>, dim3(blocks_for(s.n, 64)), dim3(64), 0, (hipStream_t)stream, s,
+                       steps, d_rng, d_actions);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_seed_sampler(size_t n, uint32_t seed, uint32_t *d_rng, void *stream) {

@@ -175,6 +175,7 @@ class Runner {
   }
   void rollout(int steps) { check(cog_runner_rollout(h_, steps)); }
   void set_timing(bool on) { check(cog_runner_set_timing(h_, on)); }
+  void set_chunk(int k) { check(cog_runner_set_chunk(h_, k)); }
   py::tuple kernel_time() {
     double ms = 0;
     uint64_t k = 0;
@@ -310,5 +311,6 @@ PYBIND11_MODULE(_city_of_gold, m) {
       .def("sync", &Runner::sync)
       .def("rollout", &Runner::rollout, "steps"_a)
       .def("set_timing", &Runner::set_timing, "enable"_a)
+      .def("set_chunk", &Runner::set_chunk, "steps_per_launch"_a)
       .def("kernel_time", &Runner::kernel_time);
 }

@@ -146,6 +146,9 @@ COG_API int cog_runner_sample(cog_runner *r);    /* enqueue sample(selected mask
 COG_API int cog_runner_step(cog_runner *r);      /* enqueue step(sampler actions); fuses a pending sample */
 COG_API int cog_runner_sync(cog_runner *r);      /* wait; refresh host views unless DEVICE_VIEWS */
 COG_API int cog_runner_rollout(cog_runner *r, int steps);   /* enqueue steps x (sample; step) */
+/* rollout() steps per kernel launch: 1 = one launch per step; K > 1 = a persistent kernel runs
+   K x (sample; step) per launch, storing every step's outputs as a single step does */
+COG_API int cog_runner_set_chunk(cog_runner *r, int steps_per_launch);
 COG_API int cog_runner_set_timing(cog_runner *r, int enable);
 /* device time of the fused launches since enabled: HIP events bracket each step() launch and each
    rollout() batch on the env's stream; *launches = fused launches covered */

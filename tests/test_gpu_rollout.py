@@ -1,0 +1,88 @@
+"""GPU: the persistent rollout kernel (runner.set_chunk(K > 1): K x (sample; step) per launch, state
+kept on-chip between steps, every step's outputs stored) against the oracle and against one
+launch per step.  Bit-exact over named fields."""
+import numpy as np
+import pytest
+
+import pyoracle as po
+
+pytestmark = pytest.mark.gpu
+
+
+def run(cg, n, seed, n_players, diff, max_steps, steps, chunk, stored):
+    env = cg.vec.get_vec_env(n)()
+    smp = cg.vec.get_vec_sampler(n)(seed)
+    env.reset(seed, n_players, 3, cg.Difficulty(diff), max_steps, False)
+    runner = cg.vec.get_runner(n)(env, smp, None, stored_masks=stored, device_views=True)
+    runner.set_chunk(chunk)
+    runner.rollout(steps)
+    runner.sync()
+    env.sync_host()
+    return env, smp, runner
+
+
+@pytest.mark.parametrize("chunk", [5, 64])
+def test_rollout_stored_resets_against_oracle(cg, chunk):
+    """Full dynamics (moves, shop, specials) with many auto-resets inside one launch."""
+    n, steps = 1024, 300
+    env, smp, _ = run(cg, n, 31337, 4, 2, 25, steps, chunk, True)
+    orc, osm = po.OracleVec(n), po.OracleSampler(n, 31337)
+    orc.reset(31337, 4, 3, 2, 25)
+    for _ in range(steps):
+        osm.sample(po.stored_masks(orc))
+        orc.step(osm.actions)
+    for nm in ("observations", "selected_action_masks", "infos"):
+        assert po.named_equal(getattr(env, nm), getattr(orc, nm)) is None, nm
+    assert np.array_equal(env.rewards, orc.rewards)
+    assert np.array_equal(env.dones, orc.dones)
+    assert np.array_equal(env.agent_selection, orc.agent_selection)
+    haz, per = env.hazards()
+    assert np.array_equal(per, orc.flags())
+
+
+@pytest.mark.parametrize("n_players", [2, 3])
+def test_rollout_fewer_players_against_oracle(cg, n_players):
+    n, steps = 512, 200
+    env, smp, _ = run(cg, n, 4242, n_players, 1, 100000, steps, 50, False)
+    orc, osm = po.OracleVec(n), po.OracleSampler(n, 4242)
+    orc.reset(4242, n_players, 3, 1, 100000)
+    for _ in range(steps):
+        osm.sample(orc.selected_action_masks)
+        orc.step(osm.actions)
+    for nm in ("observations", "selected_action_masks", "infos"):
+        assert po.named_equal(getattr(env, nm), getattr(orc, nm)) is None, nm
+    assert np.array_equal(env.agent_selection, orc.agent_selection)
+
+
+def test_rollout_equals_per_step_launches_at_c5_size(cg):
+    """C5 shape (65,536 envs, 4p, HARD): chunked rollout == one launch per step, byte for byte
+    over every device buffer a step writes."""
+    n, steps = 65536, 120
+    a, sa, _ = run(cg, n, 12345, 4, 2, 100000, steps, 40, False)
+    b, sb, _ = run(cg, n, 12345, 4, 2, 100000, steps, 1, False)
+    for nm in ("observations", "selected_action_masks", "infos", "rewards", "dones", "agent_selection"):
+        assert np.array_equal(getattr(a, nm).view(np.uint8), getattr(b, nm).view(np.uint8)), nm
+
+
+def test_rollout_interleaves_with_host_steps(cg):
+    """A chunked rollout, then host-API sample/step, then a rollout again: one consistent state."""
+    n = 256
+    env, smp, runner = run(cg, n, 99, 4, 2, 40, 37, 16, True)
+    orc, osm = po.OracleVec(n), po.OracleSampler(n, 99)
+    orc.reset(99, 4, 3, 2, 40)
+    for _ in range(37):
+        osm.sample(po.stored_masks(orc))
+        orc.step(osm.actions)
+    for _ in range(5):                                     # host API in between
+        smp.sample(po.stored_masks(env))
+        osm.sample(po.stored_masks(orc))
+        env.step(smp.get_actions())
+        orc.step(osm.actions)
+    runner.rollout(29)
+    runner.sync()
+    env.sync_host()
+    for _ in range(29):
+        osm.sample(po.stored_masks(orc))
+        orc.step(osm.actions)
+    for nm in ("observations", "selected_action_masks", "infos"):
+        assert po.named_equal(getattr(env, nm), getattr(orc, nm)) is None, nm

@@ -1,5 +1,5 @@
 // Diagnostic only: the fused step kernel built with -DCOG_STAMPS (per-wave s_memtime at phase
-// boundaries of staged_step) on the bench workload; prints mean cycles per phase.
+// boundaries of env_step_lane) on the bench workload; prints mean cycles per phase.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DCOG_STAMPS -Iinclude \
 //         -Igym-eldorado_amd/csrc tools/stamp_step.cpp -o tools/stamp_step
 #include "../gym-eldorado_amd/csrc/cog_engine.hip"
@@ -28,11 +28,9 @@ int main(int argc, char **argv) {
   env->s.stamps = d;
   std::vector<unsigned long long> h(waves * K);
   // phase j = ticks from the previous stamp that was reached to stamp j
-  const char *names[K] = {"", "stage-in (2 dependent rounds, cooperative)", "sample (5 masked picks)",
-                          "step: action branch", "step: mip + turn end (discard, draw)",
-                          "step: mover's cell reload", "step: update_observation masks",
-                          "step: special / done check", "", "", "step: rest", "auto-reset + plan",
-                          "cooperative stores issued", "", "", ""};
+  const char *names[K] = {"", "loads (2 rounds) + sample + unpack", "repack registers",
+                          "game logic (registers)", "compare + stores issued", "finish / done / reset",
+                          "wave encode", "", "", "", "", "", "", "", "", ""};
   std::vector<double> ph[K], tot;
   for (int t = 0; t < steps; t++) {
     if (hipMemset(d, 0, waves * K * sizeof(unsigned long long)) != hipSuccess) return 1;
