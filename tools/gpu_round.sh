@@ -13,7 +13,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
     > "$OUT/tests.log" 2>&1 && \
 timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" && \
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
-    -- python3 "$ROOT/bench.py" --steps 2000 --warmup 200 --no-cpu-baseline) \
+    -- python3 "$ROOT/bench.py" --steps 2000 --warmup 1000 --no-cpu-baseline) \
     > "$OUT/prof_bench.json" 2> "$OUT/prof.err" && \
 tools/pmc_passes.sh "$TAG/pmc" 2000
 rc=$?

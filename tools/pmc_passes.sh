@@ -11,7 +11,7 @@ BENCH="$PWD/bench.py"
 run() {   # name, counters...
   local name=$1; shift
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/$name" -o run \
-      --pmc "$@" -- python3 "$BENCH" --profile-steps "$STEPS" --warmup 20 --no-cpu-baseline) \
+      --pmc "$@" -- python3 "$BENCH" --profile-steps "$STEPS" --warmup 0 --no-cpu-baseline) \
       > "$OUT/$name.log" 2>&1
 }
 run sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS && \

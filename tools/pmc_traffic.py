@@ -4,7 +4,7 @@ FETCH_SIZE reports half the bytes of wide (16 B/lane) reads, so it is doubled; W
 exact for 16-B-per-lane stores.  Writes profiles/pmc_traffic.json, stamped with the hash of the
 engine source so that bench.py reports `traffic` only for the kernel version it measures.
 
-    python tools/pmc_traffic.py gpurun_out/<tag>/pmc [envs_per_launch]
+    python tools/pmc_traffic.py gpurun_out/<tag>/pmc [envs_per_launch] [rollout steps per launch]
 """
 import hashlib
 import json
@@ -15,7 +15,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import pmc_summary  # noqa: E402
 
-KERNELS = {"cog::k_sample_step": "k_sample_step", "void cog::k_encode_lds<true>": "k_encode"}
+# kernel -> (short name, steps per launch key)
+KERNELS = {"void cog::k_env_rollout<0>": "k_env_rollout", "void cog::k_env_step<0>": "k_env_step",
+           "void cog::k_encode_lds<true>": "k_encode"}
 
 
 def engine_hash():
@@ -26,7 +28,7 @@ def engine_hash():
     return h.hexdigest()[:16]
 
 
-def main(d, envs=65536):
+def main(d, envs=65536, chunk=1000):
     tmp = os.path.join(d, "summary.json")
     pmc_summary.main(d, tmp, quiet=True)
     with open(tmp) as f:
@@ -38,7 +40,8 @@ def main(d, envs=65536):
             continue
         rd = 2.0 * res[k]["FETCH_SIZE"] * 1024
         wr = res[k]["WRITE_SIZE"] * 1024
-        out[short] = {"envs_per_launch": envs, "read_bytes": rd, "write_bytes": wr, "bytes_per_launch": rd + wr,
+        spl = chunk if short == "k_env_rollout" else 1
+        out[short] = {"envs_per_launch": envs, "steps_per_launch": spl, "read_bytes": rd, "write_bytes": wr, "bytes_per_launch": rd + wr,
                       "dispatches": res[k]["dispatches"],
                       "l2_hit": res[k].get("TCC_HIT_sum", 0) / max(1.0, res[k].get("TCC_HIT_sum", 0) + res[k].get("TCC_MISS_sum", 0))}
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
@@ -47,4 +50,4 @@ def main(d, envs=65536):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 65536)
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 65536, int(sys.argv[3]) if len(sys.argv) > 3 else 1000)
