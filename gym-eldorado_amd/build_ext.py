@@ -27,7 +27,7 @@ LIB = os.path.join(OUT, "libcog_hip.so")
 EXT = os.path.join(OUT, "_city_of_gold" + sysconfig.get_config_var("EXT_SUFFIX"))
 
 ENGINE_SRCS = [os.path.join(CSRC, f) for f in ("cog_engine.hip", "cog_abi.cpp")]
-ENGINE_DEPS = ENGINE_SRCS + [os.path.join(CSRC, f) for f in ("cog_engine.h", "cog_tables.h")] + [
+ENGINE_DEPS = ENGINE_SRCS + [os.path.join(CSRC, f) for f in ("cog_engine.h", "cog_tables.h", "cog_rng.h")] + [
     os.path.join(INCLUDE, f) for f in ("cog.h", "cog_types.h")]
 EXT_SRCS = [os.path.join(CSRC, "pybind_module.cpp")]
 

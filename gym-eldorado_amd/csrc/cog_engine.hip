@@ -24,6 +24,7 @@
 
 #include "cog_engine.h"
 #include "cog_tables.h"
+#include "cog_rng.h"
 
 #define DEV __device__ __forceinline__
 
@@ -46,6 +47,31 @@ DEV unsigned long long stamp_clock() {
 #define STAMP(s, k) do { } while (0)
 #endif
 #define STAMP_AT(k) STAMP(e, k)     // inside step functions: Ctx carries the stamp buffer
+// per-phase tick accumulators (diagnostic builds): PH(k) charges the ticks since the previous
+// PH to phase k; PH_FLUSH writes this wave's totals to the stamp buffer.  step_regs takes the
+// accumulator as an extra parameter (PH_PARAM / PH_PASS) in those builds only.
+#ifdef COG_STAMPS
+struct PhAcc {
+  unsigned long long acc[16];
+  unsigned long long last;
+};
+#define PH_DECL PhAcc ph_ = {}; ph_.last = stamp_clock()
+#define PH(k) do { const unsigned long long t_ = stamp_clock(); ph_.acc[k] += t_ - ph_.last; ph_.last = t_; } while (0)
+#define PH_PARAM , PhAcc &ph_
+#define PH_PASS , ph_
+#define PH_FLUSH(s)                                                                         \
+  do {                                                                                      \
+    if ((s).stamps && (threadIdx.x & 63) == 0)                                              \
+      for (int k_ = 0; k_ < 16; k_++)                                                       \
+        (s).stamps[((size_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 16 + k_] = ph_.acc[k_]; \
+  } while (0)
+#else
+#define PH_DECL do { } while (0)
+#define PH(k) do { } while (0)
+#define PH_PARAM
+#define PH_PASS
+#define PH_FLUSH(s) do { } while (0)
+#endif
 
 namespace cog {
 
@@ -68,30 +94,7 @@ __constant__ int8_t c_opts_lt[1] = {-3};
 // shop slots that start in the market (cards.cpp:85-92 / 94-100): slots 0,1,5,7,9,12
 constexpr uint32_t kInMarket0 = (1u << 0) | (1u << 1) | (1u << 5) | (1u << 7) | (1u << 9) | (1u << 12);
 
-// ------------------------------------------------------------------------------------------
-// RNG: minstd_rand0 and libstdc++ uniform_int_distribution<size_t> downscaling
-// ------------------------------------------------------------------------------------------
-DEV uint32_t mr_seed(uint64_t s) {
-  uint32_t x = (uint32_t)(s % 2147483647ull);
-  return x == 0 ? 1u : x;
-}
-DEV uint32_t mr_next(uint32_t &x) {
-  const uint64_t p = (uint64_t)x * 16807u;                 // < 2^46
-  uint32_t r = (uint32_t)(p & 0x7fffffffu) + (uint32_t)(p >> 31);
-  r = r >= 0x7fffffffu ? r - 0x7fffffffu : r;
-  x = r;
-  return r;
-}
-// uniform integer in [0, k-1], k >= 1 (uniform_int_distribution<size_t>(0, k-1))
-DEV uint32_t uid(uint32_t &x, uint32_t k) {
-  const uint32_t scaling = 2147483645u / k;
-  const uint32_t past = k * scaling;
-  uint32_t r;
-  do {
-    r = mr_next(x) - 1u;
-  } while (r >= past);
-  return r / scaling;
-}
+// RNG (minstd_rand0 + libstdc++ uniform_int_distribution): cog_rng.h
 
 // ------------------------------------------------------------------------------------------
 // per-env context
@@ -872,7 +875,7 @@ DEV uint32_t nth_set_bit(uint32_t m, uint32_t j) {        // index of the j-th (
 DEV uint8_t pick(uint32_t &rng, uint32_t m) {
   const uint32_t k = __popc(m);
   if (!k) return 0;
-  return (uint8_t)nth_set_bit(m, uid(rng, k));
+  return (uint8_t)nth_set_bit(m, uid_small(rng, k));      // k <= 22: division-free
 }
 DEV void sample_heads(const Heads &h, uint32_t &rng, uint8_t out[5]) {
   out[0] = pick(rng, h.play);
@@ -939,6 +942,15 @@ DEV void dk_put(uint32_t *d, int b, uint32_t v) {
   const int sh = 8 * (b & 3);
   d[b >> 2] = (d[b >> 2] & ~(0xffu << sh)) | ((v & 0xffu) << sh);
 }
+DEV uint32_t add8(uint32_t x, uint32_t y) {                // byte-wise x + y, each byte mod 256
+  return ((x & 0x7f7f7f7fu) + (y & 0x7f7f7f7fu)) ^ ((x ^ y) & 0x80808080u);
+}
+DEV uint32_t fsh8(uint32_t hi, uint32_t lo, int nb) {      // bytes nb .. nb+3 of the pair lo:hi
+  return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)nb);
+}
+DEV uint32_t bcast8(uint32_t v) { return __builtin_amdgcn_perm(0u, v, 0u); }   // byte 0 x 4
+DEV uint32_t sum8(uint32_t x, uint32_t acc) { return __builtin_amdgcn_sad_u8(x, 0u, acc); }
+
 template <int LO, int HI>                                  // byte index in [LO, HI]
 DEV uint32_t dk_getv(const uint32_t *d, int b) {
   const int q = b >> 2;
@@ -1038,33 +1050,39 @@ struct RegEnv {
     return (uint8_t)(v >> (8 * dir));
   }
 
-  // Deck::discard_all_active + discard_all_played (cards.cpp:219-232)
+  // Deck::discard_all_active + discard_all_played (cards.cpp:219-232): discard += active + played,
+  // four types per dword (active and played re-aligned to the discard pile's dword grid)
   DEV void discard_all() {
+    uint32_t D[6];
 #pragma unroll
-    for (int k = 0; k < COG_N_CARDTYPES; k++) {
-      const uint32_t a = dk_get(d, COG_DECK_ACTIVE + k), p = dk_get(d, COG_DECK_PLAYED + k);
-      dk_put(d, COG_DECK_DISCARD + k, dk_get(d, COG_DECK_DISCARD + k) + a + p);
-      dk_put(d, COG_DECK_ACTIVE + k, 0u);
-      dk_put(d, COG_DECK_PLAYED + k, 0u);
-    }
+    for (int q = 0; q < 6; q++)
+      D[q] = add8(add8(d[21 + q], fsh8(d[11 + q], d[10 + q], 2)), fsh8(d[16 + q], d[15 + q], 3));
+#pragma unroll
+    for (int q = 0; q < 5; q++) d[21 + q] = D[q];
+    d[26] = (d[26] & 0xffffff00u) | (D[5] & 0xffu);        // discard[20]; bytes 105.. are padding
+    d[10] &= 0x0000ffffu;                                  // active[0..1] ..
+#pragma unroll
+    for (int q = 11; q < 21; q++) d[q] = 0u;               // .. played[20]: bytes 42..83 = 0
   }
-  // Deck::move_discard_to_draw (cards.cpp:234-240)
+  // Deck::move_discard_to_draw (cards.cpp:234-240): both piles start on a dword
   DEV void move_discard_to_draw() {
-    uint32_t nd = P.n_in_draw;
+    uint32_t n = P.n_in_draw;
 #pragma unroll
-    for (int k = 0; k < COG_N_CARDTYPES; k++) {
-      const uint32_t v = dk_get(d, COG_DECK_DISCARD + k);
-      dk_put(d, COG_DECK_DRAW + k, dk_get(d, COG_DECK_DRAW + k) + v);
-      nd += v;
-      dk_put(d, COG_DECK_DISCARD + k, 0u);
+    for (int q = 0; q < 5; q++) {
+      n = sum8(d[21 + q], n);
+      d[q] = add8(d[q], d[21 + q]);
+      d[21 + q] = 0u;
     }
-    P.n_in_draw = nd & 0xffu;
+    const uint32_t last = d[26] & 0xffu;                   // discard[20] -> draw[20]
+    d[5] = (d[5] & 0xffffff00u) | ((d[5] + last) & 0xffu);
+    d[26] &= 0xffffff00u;
+    P.n_in_draw = (n + last) & 0xffu;
   }
-  DEV uint32_t hand_bits() const {
+  DEV uint32_t hand_bits() const {                         // hand[k] > 0 for k < 21
     uint32_t h = 0;
 #pragma unroll
-    for (int k = 0; k < COG_N_CARDTYPES; k++) h |= (dk_get(d, COG_DECK_HAND + k) != 0u ? 1u : 0u) << k;
-    return h;
+    for (int q = 0; q < 6; q++) h |= bools4(fsh8(d[6 + q], d[5 + q], 1)) << (4 * q);
+    return h & 0x1fffffu;
   }
   DEV void enable_playing() {                              // player.cpp:198-206
     const uint32_t h = hand_bits();
@@ -1072,23 +1090,58 @@ struct RegEnv {
     sel.play = 1u | (h << 1);
     sel.spec = 1u | ((h & kSpecialBits) << 1);
   }
-  // Deck::draw (cards.cpp:183-211); n_in_draw == sum(draw[]) mod 256 (every Deck operation
-  // keeps it), so the scan ends inside the pile; the guard only raises the hazard flag
+  // Deck::draw (cards.cpp:183-211).  n_in_draw == sum(draw[]) mod 256 (every Deck operation keeps
+  // it), so the scan for the t-th card ends inside the pile.  While the pile holds < 128 cards
+  // (always in valid play) the scan runs on byte-wise prefix sums, four types per dword: the card
+  // is the number of types whose prefix sum is <= t.  Otherwise -- stale-mask driving can wrap a
+  // count to 255 (Q23) -- card by card, as the reference scans (the guard only raises the flag).
   DEV void draw(uint32_t n) {
     if (P.n_in_draw < n) move_discard_to_draw();
     if (n > P.n_in_draw) n = P.n_in_draw;
-    for (uint32_t i = 0; i < n; i++) {
-      const uint32_t t = uid(rng, P.n_in_draw);
-      uint32_t c = pile_scan<COG_DECK_DRAW>(d, t);
-      if (c >= COG_N_CARDTYPES) {
-        flags |= F_SCAN_OVER;
-        c = COG_N_CARDTYPES - 1;
+    uint32_t pre[6], carry = 0;
+#pragma unroll
+    for (int q = 0; q < 6; q++) {                          // pre[q] byte j: draw[0] + .. + draw[4q+j]
+      const uint32_t x = q < 5 ? d[q] : (d[5] & 0xffu);
+      const uint32_t p1 = x + (x << 8);
+      pre[q] = p1 + (p1 << 16) + bcast8(carry);
+      carry = pre[q] >> 24;
+    }
+    uint32_t total = d[5] & 0xffu;                         // exact (no u8 wrap) pile total
+#pragma unroll
+    for (int q = 0; q < 5; q++) total = sum8(d[q], total);
+    if (total == P.n_in_draw && total < 128u) {            // every prefix sum fits in 7 bits
+      for (uint32_t i = 0; i < n; i++) {
+        const uint32_t T = bcast8(uid_fast(rng, P.n_in_draw) + 1u);
+        uint32_t c = 0;
+#pragma unroll
+        for (int q = 0; q < 6; q++)                        // bytes with prefix <= t: bit 7 clear
+          c += __popc(~((pre[q] | 0x80808080u) - T) & (q < 5 ? 0x80808080u : 0x80u));
+        const int qc = (int)(c >> 2);
+        const uint32_t sh = 8u * (c & 3u);
+#pragma unroll
+        for (int q = 0; q < 6; q++) {
+          pre[q] -= q > qc ? 0x01010101u : (q == qc ? 0x01010101u << sh : 0u);
+          d[q] -= q == qc ? 1u << sh : 0u;                 // draw[c] >= 1: no borrow
+        }
+        P.n_in_draw = (P.n_in_draw - 1) & 0xffu;
+        pile_add<COG_DECK_HAND>(d, (int)c, 1u);
+        sel.play |= 1u << (c + 1);
+        sel.spec = set_bit(sel.spec, (int)c + 1, is_special((int)c));
       }
-      pile_add<COG_DECK_DRAW>(d, (int)c, 0xffu);
-      P.n_in_draw = (P.n_in_draw - 1) & 0xffu;
-      pile_add<COG_DECK_HAND>(d, (int)c, 1u);
-      sel.play |= 1u << (c + 1);
-      sel.spec = set_bit(sel.spec, (int)c + 1, is_special((int)c));
+    } else {
+      for (uint32_t i = 0; i < n; i++) {
+        const uint32_t t = uid_fast(rng, P.n_in_draw);
+        uint32_t c = pile_scan<COG_DECK_DRAW>(d, t);
+        if (c >= COG_N_CARDTYPES) {
+          flags |= F_SCAN_OVER;
+          c = COG_N_CARDTYPES - 1;
+        }
+        pile_add<COG_DECK_DRAW>(d, (int)c, 0xffu);
+        P.n_in_draw = (P.n_in_draw - 1) & 0xffu;
+        pile_add<COG_DECK_HAND>(d, (int)c, 1u);
+        sel.play |= 1u << (c + 1);
+        sel.spec = set_bit(sel.spec, (int)c + 1, is_special((int)c));
+      }
     }
     P.n_in_hand = (P.n_in_hand + n) & 0xffu;
   }
@@ -1115,7 +1168,7 @@ struct RegEnv {
       n = avail;
     }
     for (uint32_t i = 0; i < n; i++) {
-      const uint32_t t = uid(rng, avail - i);
+      const uint32_t t = uid_fast(rng, avail - i);
       uint32_t s = 0, c = 0;
 #pragma unroll
       for (int k = COG_DECK_ACTIVE; k < 105; k++) {
@@ -1217,7 +1270,7 @@ DEV uint2 cells_at(const uint8_t *cgrid, const uint4 &g2, int lx, int ly) {
 
 // cog_env::step (environment.cpp:91-224) for the acting player ag == agent, every action kind.
 // Returns true when the episode ends (finish_episode runs on the stored state afterwards).
-DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i, int na) {
+DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i, int na PH_PARAM) {
   const int ag = (int)R.agent();
   PState &P = R.P;
   const uint32_t info = ((R.info_steps >> (8 * ag)) + 1u) & 0xffu;   // Info steps_taken (u8)
@@ -1325,6 +1378,7 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
       R.enable_playing();
     }
   }
+  PH(8);
   if (P.mip && !a_move) {                                  // the move HEAD, whatever was taken
     P.mip = 0;
     r0 = r1 = r2 = 0.f;
@@ -1334,7 +1388,9 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
     P.n_active = 0;                                        // Player::end_turn (player.cpp:170-180)
     R.discard_all();
     const int n_draw = COG_HAND_SIZE - (int)P.n_in_hand;
+    PH(9);
     if (n_draw > 0) R.draw((uint32_t)n_draw);
+    PH(10);
     R.sta = R.sel;                                         // save_actionmask
     R.set_agent((uint32_t)na);
     if (na == ag) R.sel = R.sta;                           // load_actionmask
@@ -1352,6 +1408,7 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
                          (int8_t)((R.g2.w >> (8 * ag)) & 0xffu));
     if (na == ag) R.cells_n = R.cells_a;
   }
+  PH(11);
   const uint2 cc = cur_is_ag ? R.cells_a : R.cells_n;
   Heads &stc = cur_is_ag ? R.sta : R.stn;
   uint32_t mv = 1u, sp = 1u;                               // update_observation (:252-279)
@@ -1359,6 +1416,7 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
   else if (phase == COG_PHASE_BUYING) sp = R.shop_bits(r2);
   stc.move = mv;
   stc.shop = sp;
+  PH(12);
   if (special != COG_SPECIAL_NONE) {
     R.apply_special(special, stc);
     return false;
@@ -1444,9 +1502,8 @@ DEV void store_changes(const DevState &s, size_t i, int ag, int na, const Snap &
   if (ne4(g0n, S.g0)) pw[0] = g0n;
   if (ne4(g1n, S.g1)) pw[1] = g1n;
   if (R.moved) pw[2] = R.g2;
-  if (R.info_steps != S.info_steps) reinterpret_cast<uint32_t *>(pw + 3)[0] = R.info_steps;
-  const uint4 pl = pack_player(R.P);
-  if (ne4(pl, S.pla)) pw[4 + ag] = pl;
+  reinterpret_cast<uint32_t *>(pw + 3)[0] = R.info_steps;  // both change on every step
+  pw[4 + ag] = pack_player(R.P);
   if (R.moved) reinterpret_cast<uint2 *>(pw + 8)[ag] = R.cells_a;
 #pragma unroll
   for (int k = 0; k < 3; k++) {
@@ -1492,10 +1549,12 @@ DEV void step_action(RegEnv &R, const uint8_t *act_in, size_t i, uint32_t &srng,
 
 // episode end + dones[i] + auto-reset (environment.cpp:187-207, vec_environment.h:56-59) on the
 // stored state; returns true when the env's map was regenerated (the wave encodes it)
-DEV bool end_of_step(const DevState &s, size_t i, bool was_done, bool finish, uint32_t &agent) {
+// `out` caches (dones[i] | agent_selection[i] << 8) as last stored (~0u: unknown), so bytes that
+// already hold the value are not stored again
+DEV bool end_of_step(const DevState &s, size_t i, bool was_done, bool finish, uint32_t &agent, uint32_t &out) {
   if (finish) finish_episode(make_ctx(s, i));
   const bool done = was_done || finish;
-  s.done[i] = done ? 1 : 0;                                // dones[i] before the auto-reset
+  if ((out & 0xffu) != (done ? 1u : 0u)) s.done[i] = done ? 1 : 0;   // dones[i] before the auto-reset
   bool enc = false;
   if (done) {
     Ctx e = make_ctx(s, i);
@@ -1510,7 +1569,8 @@ DEV bool end_of_step(const DevState &s, size_t i, bool was_done, bool finish, ui
     sync_heads(s, i);
     agent = e.pv->agent;
   }
-  s.agent[i] = (uint8_t)agent;
+  if (((out >> 8) & 0xffu) != (agent & 0xffu)) s.agent[i] = (uint8_t)agent;
+  out = (done ? 1u : 0u) | (agent & 0xffu) << 8;
   return enc;
 }
 
@@ -1519,6 +1579,7 @@ DEV bool end_of_step(const DevState &s, size_t i, bool was_done, bool finish, ui
 template <int SRC>
 DEV bool env_step_lane(const DevState &s, size_t i, const uint8_t *act_in, uint32_t *rngs, uint8_t *actions_out) {
   STAMP(s, 0);
+  PH_DECL;
   Snap S;
   RegEnv R;
   load_env(s, i, S);
@@ -1537,13 +1598,13 @@ DEV bool env_step_lane(const DevState &s, size_t i, const uint8_t *act_in, uint3
   }
   STAMP(s, 1);
   const bool was_done = R.done() != 0u;
-  const bool finish = !was_done && step_regs(R, act, s, i, na);
+  const bool finish = !was_done && step_regs(R, act, s, i, na PH_PASS);
   if (finish) R.set_done(1u);
   STAMP(s, 2);
   store_changes(s, i, ag, na, S, R);
   STAMP(s, 3);
-  uint32_t agent = R.agent();
-  const bool enc = end_of_step(s, i, was_done, finish, agent);
+  uint32_t agent = R.agent(), out = ~0u;
+  const bool enc = end_of_step(s, i, was_done, finish, agent, out);
   STAMP(s, 4);
   return enc;
 }
@@ -1601,12 +1662,13 @@ __global__ void __launch_bounds__(64) k_env_rollout(DevState s, int steps, uint3
   const bool live = i0 < s.n;
   const size_t i = live ? i0 : 0;
   Snap S;
-  uint32_t srng = 0;
+  uint32_t srng = 0, out = ~0u;                           // out: end_of_step's output cache
   if (live) {
     load_env(s, i, S);
     lds_fill_players(L, s, i, l);
     srng = rngs[i];
   }
+  PH_DECL;
   for (int t = 0; t < steps; t++) {
     bool enc = false;
     if (live) {
@@ -1616,15 +1678,19 @@ __global__ void __launch_bounds__(64) k_env_rollout(DevState s, int steps, uint3
       const int na = ag + 1 >= (int)R.n_players() ? 0 : ag + 1;
       lds_players(L, l, ag, na, S);
       uint8_t act[5];
+      PH(0);
       if (SRC == MASK_SELECTED) step_action<SRC>(R, nullptr, i, srng, act);
       regs_players(R, S);
       if (SRC == MASK_STORED) step_action<SRC>(R, nullptr, i, srng, act);
       rngs[i] = srng;
       store_action(actions_out + i * COG_ACTION_BYTES, act);
+      PH(1);
       const bool was_done = R.done() != 0u;
-      const bool finish = !was_done && step_regs(R, act, s, i, na);
+      const bool finish = !was_done && step_regs(R, act, s, i, na PH_PASS);
       if (finish) R.set_done(1u);
+      PH(2);
       store_changes(s, i, ag, na, S, R);
+      PH(3);
       // the next step's image: registers (env level) and this wave's LDS (player level)
       S.g0 = make_uint4(R.rng, R.seed, R.max_steps, R.turn_counter);
       S.g1 = make_uint4(R.g1x, R.g1y, R.in_market, R.flags);
@@ -1638,15 +1704,19 @@ __global__ void __launch_bounds__(64) k_env_rollout(DevState s, int steps, uint3
       if (na != ag) L.heads[na][l] = mbits_u4(bits_of(R.stn));
 #pragma unroll
       for (int k = 0; k < 7; k++) L.deck[ag][k][l] = make_uint4(R.d[4 * k], R.d[4 * k + 1], R.d[4 * k + 2], R.d[4 * k + 3]);
+      PH(4);
       uint32_t agent = R.agent();
-      enc = end_of_step(s, i, was_done, finish, agent);
+      enc = end_of_step(s, i, was_done, finish, agent, out);
       if (was_done || finish) {                            // reset: reload from the stored state
         load_env(s, i, S);
         lds_fill_players(L, s, i, l);
       }
+      PH(5);
     }
     wave_encode(s, i, enc);                                // converged: the whole wave encodes
+    PH(6);
   }
+  PH_FLUSH(s);
 }
 
 __global__ void __launch_bounds__(256) k_sample(size_t n, const uint8_t *__restrict__ masks,

@@ -1,0 +1,86 @@
+"""CPU: the kernels' uniform_int_distribution variants (gym-eldorado_amd/csrc/cog_rng.h: uid_fast
+with one division, uid_small with none) against the libstdc++ formula they replace (uid), on the
+boundary cases of every k the engine uses -- each quotient boundary j*s-1, j*s, the rejection
+boundary past-1, past and the range end -- and on random states.  The header is plain integer
+code; g++ builds it here after defining COG_HD."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "gym-eldorado_amd", "csrc")
+P = 2 ** 31 - 1
+RANGE = 2147483645
+
+HARNESS = r"""
+#define COG_HD static inline
+#include "cog_rng.h"
+extern "C" void run(const uint32_t *x0, const uint32_t *k, uint32_t n, int which, uint32_t *out, uint32_t *xout) {
+  for (uint32_t i = 0; i < n; i++) {
+    uint32_t x = x0[i];
+    out[i] = which == 0 ? cog::uid(x, k[i]) : which == 1 ? cog::uid_fast(x, k[i]) : cog::uid_small(x, k[i]);
+    xout[i] = x;
+  }
+}
+"""
+
+
+@pytest.fixture(scope="module")
+def lib(tmp_path_factory):
+    d = tmp_path_factory.mktemp("rng")
+    src, so = d / "harness.cpp", d / "librng.so"
+    src.write_text(HARNESS)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", f"-I{CSRC}", str(src), "-o", str(so)], check=True)
+    lib = ctypes.CDLL(str(so))
+    lib.run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    return lib
+
+
+def call(lib, which, x0, k):
+    x0 = np.ascontiguousarray(x0, dtype=np.uint32)
+    k = np.ascontiguousarray(k, dtype=np.uint32)
+    out, xo = np.empty_like(x0), np.empty_like(x0)
+    lib.run(x0.ctypes.data, k.ctypes.data, len(x0), which, out.ctypes.data, xo.ctypes.data)
+    return out, xo
+
+
+def state_before(r):
+    """minstd_rand0 state whose next draw gives urng() - 1 == r."""
+    inv = pow(16807, -1, P)
+    return (r + 1) * inv % P
+
+
+def boundary_cases(kmax):
+    xs, ks = [], []
+    for k in range(1, kmax + 1):
+        s = RANGE // k
+        past = k * s
+        rs = {0, 1, past - 1, past, min(past + 1, RANGE), RANGE - 1, RANGE}
+        for j in range(1, k + 1):
+            rs |= {j * s - 1, j * s, j * s + 1}
+        for r in sorted(r for r in rs if 0 <= r <= RANGE):
+            xs.append(state_before(r))
+            ks.append(k)
+    return np.array(xs), np.array(ks)
+
+
+@pytest.mark.parametrize("which,kmax", [(1, 300), (2, 31)])
+def test_boundaries(lib, which, kmax):
+    x0, k = boundary_cases(kmax)
+    ref, xref = call(lib, 0, x0, k)
+    got, xgot = call(lib, which, x0, k)
+    bad = np.nonzero((ref != got) | (xref != xgot))[0]
+    assert bad.size == 0, f"k={k[bad[:5]]} x0={x0[bad[:5]]}: {ref[bad[:5]]} vs {got[bad[:5]]}"
+
+
+@pytest.mark.parametrize("which,kmax", [(1, 255), (2, 31)])
+def test_random_states(lib, which, kmax):
+    rng = np.random.default_rng(7 + which)
+    x0 = rng.integers(1, P, size=2_000_000, dtype=np.uint64).astype(np.uint32)
+    k = rng.integers(1, kmax + 1, size=x0.size, dtype=np.uint64).astype(np.uint32)
+    ref, xref = call(lib, 0, x0, k)
+    got, xgot = call(lib, which, x0, k)
+    assert np.array_equal(ref, got) and np.array_equal(xref, xgot)

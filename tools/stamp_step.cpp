@@ -11,6 +11,7 @@
 int main(int argc, char **argv) {
   const size_t n = argc > 1 ? strtoul(argv[1], nullptr, 10) : 65536;
   const int steps = argc > 2 ? atoi(argv[2]) : 50;
+  const int chunk = argc > 3 ? atoi(argv[3]) : 1;   // > 1: the persistent rollout, per-phase totals
   cog_env *env;
   cog_sampler *smp;
   cog_runner *run;
@@ -22,6 +23,35 @@ int main(int argc, char **argv) {
   cog_runner_rollout(run, 100);
   cog_runner_sync(run);
   const size_t waves = (n + 63) / 64;
+  if (chunk > 1) {
+    unsigned long long *d;
+    constexpr int K = 16;
+    if (hipMalloc(&d, waves * K * sizeof(unsigned long long)) != hipSuccess) return 1;
+    if (hipMemset(d, 0, waves * K * sizeof(unsigned long long)) != hipSuccess) return 1;
+    env->s.stamps = d;
+    cog_runner_set_chunk(run, chunk);
+    cog_runner_rollout(run, chunk);
+    cog_runner_sync(run);
+    std::vector<unsigned long long> h(waves * K);
+    if (hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+    const char *pn[16] = {"LDS players + unpack", "sample + action/rng stores", "game logic: rest",
+                          "compare + stores", "LDS write-back", "finish / done / reset", "wave encode", "",
+                          "  logic: info, phase, action branch", "  logic: mip + end_turn discard",
+                          "  logic: draw", "  logic: mask swap, sh, moved cells", "  logic: update_observation",
+                          "", "", ""};
+    printf("rollout: s_memtime ticks per step per wave, median over waves (n=%zu, %d steps):\n", n, chunk);
+    double tot = 0;
+    for (int k = 0; k < 13; k++) {
+      if (!pn[k][0]) continue;
+      std::vector<double> v;
+      for (size_t w = 0; w < waves; w++) v.push_back((double)h[w * K + k] / chunk);
+      std::sort(v.begin(), v.end());
+      printf("  %-40s %9.0f\n", pn[k], v[v.size() / 2]);
+      tot += v[v.size() / 2];
+    }
+    printf("  %-40s %9.0f\n", "sum", tot);
+    return 0;
+  }
   constexpr int K = 16;
   unsigned long long *d;
   if (hipMalloc(&d, waves * K * sizeof(unsigned long long)) != hipSuccess) return 1;
