@@ -1181,16 +1181,26 @@ struct RegEnv {
       if (discard) dk_addv<COG_DECK_DISCARD, COG_DECK_DISCARD + 20>(d, COG_DECK_DISCARD + (int)c, 1u);
     }
   }
-  // movement mask bits 1..6 (map.cpp:369-387) + bit 0, from a player's cached neighbourhood
+  // movement mask bits 1..6 (map.cpp:369-387) + bit 0, from a player's cached neighbourhood.
+  // A hex code's low 6 bits are req * 8 + n.  The largest n each requirement meets is
+  // floor(resource) for machete / paddle / coin (r >= n, n integer) and n_active - 1 for discard
+  // / remove (n_active > n; codes 6 and 7 compare like them), none for NULL; so the hexes that
+  // can be entered form one 64-bit set over (req, n), tested once per neighbour.
   DEV uint32_t move_bits(const uint2 &cc, float r0, float r1, float r2, uint32_t n_active) {
+    if ((cc.y >> 24) & 0x7eu) flags |= F_OOB_LOOKUP;      // the lookups of cells 1..6
+    auto width = [](float r) {                             // n in [0, width) is met by r >= n
+      return (uint32_t)__builtin_amdgcn_fmed3f(floorf(r) + 1.f, 0.f, 8.f);
+    };
+    const uint32_t wa = min(n_active, 8u);
+    const uint32_t lo = __builtin_amdgcn_ubfe(0xffu, 0, width(r0)) | __builtin_amdgcn_ubfe(0xffu, 0, width(r1)) << 8 |
+                        __builtin_amdgcn_ubfe(0xffu, 0, width(r2)) << 16 | __builtin_amdgcn_ubfe(0xffu, 0, wa) << 24;
+    const uint32_t ha = __builtin_amdgcn_ubfe(0xffu, 0, wa);
+    const uint64_t ok = (uint64_t)lo | (uint64_t)(ha | ha << 16 | ha << 24) << 32;   // req 4, 6, 7
     uint32_t m = 1u;
 #pragma unroll
     for (int dir = 1; dir < 7; dir++) {
-      const uint32_t c = use_cell(cc, dir);
-      const uint32_t req = COG_HEX_REQ(c), n = COG_HEX_N(c);
-      const float r = req == 0 ? r0 : (req == 1 ? r1 : r2);
-      const bool filled = req >= COG_REQ_DISCARD ? n_active > n : r >= (float)n;
-      if (req != COG_REQ_NULL && filled) m |= 1u << dir;
+      const uint32_t idx = (dir < 4 ? cc.x >> (8 * dir) : cc.y >> (8 * (dir - 4))) & 0x3fu;
+      m |= (uint32_t)((ok >> idx) & 1u) << dir;
     }
     return m;
   }
@@ -1412,8 +1422,10 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
   const uint2 cc = cur_is_ag ? R.cells_a : R.cells_n;
   Heads &stc = cur_is_ag ? R.sta : R.stn;
   uint32_t mv = 1u, sp = 1u;                               // update_observation (:252-279)
+#ifndef COG_ABLATE_UPDOBS                                  // diagnostic timing builds only
   if (phase == COG_PHASE_MOVEMENT) mv = R.move_bits(cc, r0, r1, r2, cur_is_ag ? P.n_active : R.na_active);
   else if (phase == COG_PHASE_BUYING) sp = R.shop_bits(r2);
+#endif
   stc.move = mv;
   stc.shop = sp;
   PH(12);
@@ -1493,18 +1505,15 @@ DEV void store_mask_record(uint4 *rec, const MBits &b, uint32_t gm) {
   for (int g = 0; g < 6; g++)
     if ((gm >> g) & 1u) rec[g] = mask_granule(b, g);
 }
-// write back every granule that differs from the step-start image S (ag / na: players of S)
-DEV void store_changes(const DevState &s, size_t i, int ag, int na, const Snap &S, const RegEnv &R) {
-  uint4 *pw = reinterpret_cast<uint4 *>(s.priv + i);
+// The store phase.  Outputs -- the ObsData tail (phase / resources / shop, the acting player's
+// deck, the stored masks) and the selected_action_masks record -- are stored granule by granule
+// where they differ from the step-start image S, on every step.  Private state (EnvPriv, the
+// mask bit vectors) is stored by the single-step kernel on every step; the rollout keeps it
+// on-chip and stores it before anything reads it back (episode end, reset, end of launch).
+// A move stores the new locations at once: the next move re-reads them.
+DEV void store_outputs(const DevState &s, size_t i, int ag, int na, const Snap &S, const RegEnv &R) {
   uint8_t *ob = s.obs + i * COG_OBS_BYTES;
-  const uint4 g0n = make_uint4(R.rng, R.seed, R.max_steps, R.turn_counter);
-  const uint4 g1n = make_uint4(R.g1x, R.g1y, R.in_market, R.flags);
-  if (ne4(g0n, S.g0)) pw[0] = g0n;
-  if (ne4(g1n, S.g1)) pw[1] = g1n;
-  if (R.moved) pw[2] = R.g2;
-  reinterpret_cast<uint32_t *>(pw + 3)[0] = R.info_steps;  // both change on every step
-  pw[4 + ag] = pack_player(R.P);
-  if (R.moved) reinterpret_cast<uint2 *>(pw + 8)[ag] = R.cells_a;
+  if (R.moved) reinterpret_cast<uint4 *>(s.priv + i)[2] = R.g2;
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     const uint4 v = make_uint4(R.sh[4 * k], R.sh[4 * k + 1], R.sh[4 * k + 2], R.sh[4 * k + 3]);
@@ -1517,14 +1526,28 @@ DEV void store_changes(const DevState &s, size_t i, int ag, int na, const Snap &
     if (ne4(v, S.dk[k])) reinterpret_cast<uint4 *>(deck)[k] = v;
   }
   const MBits bs = bits_of(R.sel), ba = bits_of(R.sta), bn = bits_of(R.stn);
-  const uint32_t gs = mask_diff_granules(bs, S.sel), ga = mask_diff_granules(ba, S.sta),
-                 gn = na != ag ? mask_diff_granules(bn, S.stn) : 0u;
-  if (gs) s.heads[5 * i] = mbits_u4(bs);
-  if (ga) s.heads[5 * i + 1 + ag] = mbits_u4(ba);
-  if (gn) s.heads[5 * i + 1 + na] = mbits_u4(bn);
-  store_mask_record(reinterpret_cast<uint4 *>(s.sel + i * COG_MASK_BYTES), bs, gs);
-  store_mask_record(reinterpret_cast<uint4 *>(deck + COG_PD_MASK), ba, ga);
-  store_mask_record(reinterpret_cast<uint4 *>(deck_ptr(s, i, na) + COG_PD_MASK), bn, gn);
+  store_mask_record(reinterpret_cast<uint4 *>(s.sel + i * COG_MASK_BYTES), bs, mask_diff_granules(bs, S.sel));
+  store_mask_record(reinterpret_cast<uint4 *>(deck + COG_PD_MASK), ba, mask_diff_granules(ba, S.sta));
+  if (na != ag)
+    store_mask_record(reinterpret_cast<uint4 *>(deck_ptr(s, i, na) + COG_PD_MASK), bn, mask_diff_granules(bn, S.stn));
+}
+DEV void store_private(const DevState &s, size_t i, int ag, int na, const Snap &S, const RegEnv &R) {
+  uint4 *pw = reinterpret_cast<uint4 *>(s.priv + i);
+  const uint4 g0n = make_uint4(R.rng, R.seed, R.max_steps, R.turn_counter);
+  const uint4 g1n = make_uint4(R.g1x, R.g1y, R.in_market, R.flags);
+  if (ne4(g0n, S.g0)) pw[0] = g0n;
+  if (ne4(g1n, S.g1)) pw[1] = g1n;
+  reinterpret_cast<uint32_t *>(pw + 3)[0] = R.info_steps;  // both change on every step
+  pw[4 + ag] = pack_player(R.P);
+  if (R.moved) reinterpret_cast<uint2 *>(pw + 8)[ag] = R.cells_a;
+  const MBits bs = bits_of(R.sel), ba = bits_of(R.sta), bn = bits_of(R.stn);
+  if (mask_diff_granules(bs, S.sel)) s.heads[5 * i] = mbits_u4(bs);
+  if (mask_diff_granules(ba, S.sta)) s.heads[5 * i + 1 + ag] = mbits_u4(ba);
+  if (na != ag && mask_diff_granules(bn, S.stn)) s.heads[5 * i + 1 + na] = mbits_u4(bn);
+}
+DEV void store_changes(const DevState &s, size_t i, int ag, int na, const Snap &S, const RegEnv &R) {
+  store_outputs(s, i, ag, na, S, R);
+  store_private(s, i, ag, na, S, R);
 }
 
 // the action of this step: sampled (runner) or the host's (indices past a head are the
@@ -1642,6 +1665,21 @@ DEV void lds_fill_players(LaneLds &L, const DevState &s, size_t i, int l) {
     L.heads[p][l] = s.heads[5 * i + 1 + p];
   }
 }
+// every private record of env i (EnvPriv granules 0, 1, 3, all players, all mask bit vectors)
+// from the rollout's on-chip copies
+DEV void store_private_all(const DevState &s, size_t i, const Snap &S, const LaneLds &L, int l) {
+  uint4 *pw = reinterpret_cast<uint4 *>(s.priv + i);
+  pw[0] = S.g0;
+  pw[1] = S.g1;
+  reinterpret_cast<uint32_t *>(pw + 3)[0] = S.info_steps;
+  s.heads[5 * i] = mbits_u4(S.sel);
+#pragma unroll
+  for (int p = 0; p < 4; p++) {
+    pw[4 + p] = L.pl[p][l];
+    reinterpret_cast<uint2 *>(pw + 8)[p] = L.cells[p][l];
+    s.heads[5 * i + 1 + p] = L.heads[p][l];
+  }
+}
 DEV void lds_players(const LaneLds &L, int l, int ag, int na, Snap &S) {
   S.pla = L.pl[ag][l];
   S.pln = L.pl[na][l];
@@ -1682,14 +1720,15 @@ __global__ void __launch_bounds__(64) k_env_rollout(DevState s, int steps, uint3
       if (SRC == MASK_SELECTED) step_action<SRC>(R, nullptr, i, srng, act);
       regs_players(R, S);
       if (SRC == MASK_STORED) step_action<SRC>(R, nullptr, i, srng, act);
-      rngs[i] = srng;
       store_action(actions_out + i * COG_ACTION_BYTES, act);
       PH(1);
       const bool was_done = R.done() != 0u;
       const bool finish = !was_done && step_regs(R, act, s, i, na PH_PASS);
       if (finish) R.set_done(1u);
       PH(2);
-      store_changes(s, i, ag, na, S, R);
+#ifndef COG_ABLATE_STORES                                  // diagnostic timing builds only
+      store_outputs(s, i, ag, na, S, R);
+#endif
       PH(3);
       // the next step's image: registers (env level) and this wave's LDS (player level)
       S.g0 = make_uint4(R.rng, R.seed, R.max_steps, R.turn_counter);
@@ -1706,15 +1745,22 @@ __global__ void __launch_bounds__(64) k_env_rollout(DevState s, int steps, uint3
       for (int k = 0; k < 7; k++) L.deck[ag][k][l] = make_uint4(R.d[4 * k], R.d[4 * k + 1], R.d[4 * k + 2], R.d[4 * k + 3]);
       PH(4);
       uint32_t agent = R.agent();
-      enc = end_of_step(s, i, was_done, finish, agent, out);
-      if (was_done || finish) {                            // reset: reload from the stored state
-        load_env(s, i, S);
+      if (was_done || finish) {                            // episode end: state to HBM first
+        store_private_all(s, i, S, L, l);
+        enc = end_of_step(s, i, was_done, finish, agent, out);
+        load_env(s, i, S);                                 // reset: reload from the stored state
         lds_fill_players(L, s, i, l);
+      } else {
+        enc = end_of_step(s, i, false, false, agent, out);
       }
       PH(5);
     }
     wave_encode(s, i, enc);                                // converged: the whole wave encodes
     PH(6);
+  }
+  if (live) {                                              // private state back to HBM
+    store_private_all(s, i, S, L, l);
+    rngs[i] = srng;
   }
   PH_FLUSH(s);
 }
