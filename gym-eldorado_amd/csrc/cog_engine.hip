@@ -875,6 +875,11 @@ DEV uint32_t nth_set_bit(uint32_t m, uint32_t j) {        // index of the j-th (
 DEV uint8_t pick(uint32_t &rng, uint32_t m) {
   const uint32_t k = __popc(m);
   if (!k) return 0;
+  if (k == 1) {                                            // one candidate: a single accepted draw
+    uint32_t r = mr_next(rng) - 1u;                        // (past = range: only r == range rejects)
+    while (r >= kUrngRange) r = mr_next(rng) - 1u;
+    return (uint8_t)(__ffs(m) - 1);
+  }
   return (uint8_t)nth_set_bit(m, uid_small(rng, k));      // k <= 22: division-free
 }
 DEV void sample_heads(const Heads &h, uint32_t &rng, uint8_t out[5]) {
