@@ -279,7 +279,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_env_rollout<selected>",
+                "kernel": "k_env_rollout<selected, lean> + fix-up",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

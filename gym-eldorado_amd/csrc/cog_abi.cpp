@@ -124,7 +124,7 @@ void env_free(cog_env *e) {
   DeviceGuard g(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   void *dev[] = {e->s.obs, e->s.sel, e->s.info, e->s.rew, e->s.done, e->s.agent, e->s.priv,
-                 e->s.grid, e->s.cgrid, e->s.heads, e->s.gen, e->s.status, e->s.dirty, e->d_actions};
+                 e->s.grid, e->s.cgrid, e->s.heads, e->s.park, e->s.gen, e->s.status, e->s.dirty, e->d_actions};
   for (void *p : dev)
     if (p) (void)hipFree(p);
   void *hst[] = {e->h_obs, e->h_sel, e->h_rew, e->h_done, e->h_agent, e->h_info, e->h_status};
@@ -252,7 +252,7 @@ int cog_env_create(size_t n_envs, int device, cog_env **out) {
       (rc = dmalloc(&s.done, n)) || (rc = dmalloc(&s.agent, n)) ||
       (rc = dmalloc(&s.priv, n * sizeof(cog::EnvPriv))) ||
       (rc = dmalloc(&s.grid, n * (size_t)cog::kGridBytes)) || (rc = dmalloc(&s.cgrid, n * (size_t)COG_CELLS)) ||
-      (rc = dmalloc(&s.heads, n * 5 * sizeof(uint4))) ||
+      (rc = dmalloc(&s.heads, n * 5 * sizeof(uint4))) || (rc = dmalloc(&s.park, n * sizeof(uint32_t))) ||
       (rc = dmalloc(&s.gen, n * sizeof(cog::GenScratch))) || (rc = dmalloc(&s.status, 64)) ||
       (rc = dmalloc(&s.dirty, n * sizeof(uint32_t))) || (rc = dmalloc(&e->d_actions, n * COG_ACTION_BYTES)) ||
       (rc = hmalloc(&e->h_status, 64))) {
@@ -269,6 +269,10 @@ int cog_env_create(size_t n_envs, int device, cog_env **out) {
       env_free(e);
       return fail(COG_ERR_HIP, "hipMemsetAsync failed");
     }
+  if (hipMemsetAsync(s.park, 0xff, n * sizeof(uint32_t), e->stream) != hipSuccess) {   // nothing parked
+    env_free(e);
+    return fail(COG_ERR_HIP, "hipMemsetAsync failed");
+  }
   const uint32_t default_seed = std::random_device{}();   // cog_env() seeds from random_device
   if (cog::launch_init(s, nullptr, default_seed, e->stream) || hipStreamSynchronize(e->stream) != hipSuccess) {
     env_free(e);

@@ -96,6 +96,7 @@ struct DevState {
   GenScratch *gen;
   uint32_t *status;                  // [0] OR of error flags, [1] error count, [2] dirty count
   uint32_t *dirty;                   // [cap] envs whose map was re-generated (host view refresh)
+  uint32_t *park;                    // [n] rollout hand-over: step of a pending episode end, or ~0
   size_t first;                      // global index of env 0 (sub-range launches; dirty list ids)
   size_t cap;                        // capacity of the dirty list
   unsigned long long *stamps;        // diagnostic builds (COG_STAMPS) only: per-wave phase clocks
@@ -122,6 +123,7 @@ inline DevState sub_state(const DevState &s, size_t lo, size_t hi) {
   t.grid += lo * (size_t)kGridBytes;
   t.cgrid += lo * (size_t)COG_CELLS;
   t.heads += lo * 5;
+  t.park += lo;
   t.gen += lo;
   return t;
 }

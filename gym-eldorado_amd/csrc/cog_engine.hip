@@ -1696,30 +1696,62 @@ DEV void lds_players(const LaneLds &L, int l, int ag, int na, Snap &S) {
   for (int k = 0; k < 7; k++) S.dk[k] = L.deck[ag][k][l];
 }
 
-template <int SRC>
+// The rollout is two kernels.  k_env_rollout<SRC, false> ("lean") carries no episode-end code:
+// a lane whose env finishes (or starts done) at step t stores its state, records t in park[i]
+// and leaves the loop; the other lanes go on.  k_env_rollout<SRC, true> ("fix-up"), launched
+// right after it on the same stream, picks up exactly those envs: it completes step t's episode
+// end (finish_episode, dones, auto-reset, encode) and runs the env's remaining steps with the
+// full step (resets included).  Nothing reads the envs between the two launches, and envs are
+// independent (no barrier between the reference's workers either, runner.h:39-62), so the
+// outputs are the single-kernel ones; the lean kernel's loop drops the reset path's registers
+// (no AGPR or scratch spills: 214 VGPRs).  Lanes with nothing parked leave the fix-up at once.
+constexpr uint32_t kParkNone = ~0u, kParkFinish = 1u << 31;
+template <int SRC, bool FIX>
 __global__ void __launch_bounds__(64) k_env_rollout(DevState s, int steps, uint32_t *__restrict__ rngs,
                                                     uint8_t *__restrict__ actions_out) {
   __shared__ LaneLds L;
   const int l = threadIdx.x;
   const size_t i0 = (size_t)blockIdx.x * blockDim.x + l;
-  const bool live = i0 < s.n;
-  const size_t i = live ? i0 : 0;
+  const size_t i = i0 < s.n ? i0 : 0;
+  int t_first = 0;                                         // fix-up: this lane's first full step
+  uint32_t park = kParkNone;
+  if (FIX && i0 < s.n) park = s.park[i];
+  bool live = i0 < s.n && (!FIX || park != kParkNone);
+  if (FIX && !__builtin_amdgcn_ballot_w64(live)) return;  // (wave-uniform exit)
   Snap S;
   uint32_t srng = 0, out = ~0u;                           // out: end_of_step's output cache
+  auto next_of = [&](int a) { return a + 1 >= (int)(S.g1.x & 0xffu) ? 0 : a + 1; };   // n_players
   if (live) {
     load_env(s, i, S);
     lds_fill_players(L, s, i, l);
     srng = rngs[i];
   }
-  PH_DECL;
-  for (int t = 0; t < steps; t++) {
+  if (FIX) {                                               // step `park`'s episode end
     bool enc = false;
     if (live) {
+      s.park[i] = kParkNone;
+      t_first = (int)(park & ~kParkFinish) + 1;
+      uint32_t agent = S.g1.y & 0xffu;
+      const bool finish = (park & kParkFinish) != 0u;
+      enc = end_of_step(s, i, !finish, finish, agent, out);
+      load_env(s, i, S);                                   // reset: reload from the stored state
+      lds_fill_players(L, s, i, l);
+    }
+    wave_encode(s, i, enc);                                // converged: the whole wave encodes
+  }
+  if (live) {
+    const int ag = (int)(S.g1.y & 0xffu);
+    lds_players(L, l, ag, next_of(ag), S);
+  }
+  PH_DECL;
+  for (int t = FIX ? 1 : 0; t < steps; t++) {
+    if (!FIX && !live) break;                              // lean: a parked lane leaves the loop
+    bool enc = false;
+    if (live && t >= t_first) {
       RegEnv R;
       regs_env(R, S);
-      const int ag = (int)R.agent();
-      const int na = ag + 1 >= (int)R.n_players() ? 0 : ag + 1;
-      lds_players(L, l, ag, na, S);
+      const int ag = (int)R.agent();                       // S holds ag's and na's records: read
+      const int na = ag + 1 >= (int)R.n_players() ? 0 : ag + 1;   // at the end of the last step
       uint8_t act[5];
       PH(0);
       if (SRC == MASK_SELECTED) step_action<SRC>(R, nullptr, i, srng, act);
@@ -1752,15 +1784,24 @@ __global__ void __launch_bounds__(64) k_env_rollout(DevState s, int steps, uint3
       uint32_t agent = R.agent();
       if (was_done || finish) {                            // episode end: state to HBM first
         store_private_all(s, i, S, L, l);
+        if (!FIX) {                                        // hand the env to the fix-up kernel
+          rngs[i] = srng;
+          s.park[i] = (uint32_t)t | (finish ? kParkFinish : 0u);
+          live = false;
+          continue;
+        }
         enc = end_of_step(s, i, was_done, finish, agent, out);
         load_env(s, i, S);                                 // reset: reload from the stored state
         lds_fill_players(L, s, i, l);
+        agent = S.g1.y & 0xffu;
       } else {
         enc = end_of_step(s, i, false, false, agent, out);
       }
+      lds_players(L, l, (int)agent, next_of((int)agent), S);   // the next step's players, early:
+                                                           // the reads overlap the loop's tail
       PH(5);
     }
-    wave_encode(s, i, enc);                                // converged: the whole wave encodes
+    if (FIX) wave_encode(s, i, enc);                       // converged: the whole wave encodes
     PH(6);
   }
   if (live) {                                              // private state back to HBM
@@ -1851,12 +1892,15 @@ int launch_spin(uint32_t ns, void *stream) {
 }
 int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions, void *stream) {
   if (!s.n || steps <= 0) return 0;
-  if (mask_source == MASK_STORED)
-    hipLaunchKernelGGL(k_env_rollout<MASK_STORED>, dim3(blocks_for(s.n, 64)), dim3(64), 0, (hipStream_t)stream, s,
-                       steps, d_rng, d_actions);
-  else
-    hipLaunchKernelGGL(k_env_rollout<MASK_SELECTED>, dim3(blocks_for(s.n, 64)), dim3(64), 0, (hipStream_t)stream, s,
-                       steps, d_rng, d_actions);
+  const dim3 g(blocks_for(s.n, 64)), b(64);
+  const hipStream_t st = (hipStream_t)stream;
+  if (mask_source == MASK_STORED) {
+    hipLaunchKernelGGL((k_env_rollout<MASK_STORED, false>), g, b, 0, st, s, steps, d_rng, d_actions);
+    hipLaunchKernelGGL((k_env_rollout<MASK_STORED, true>), g, b, 0, st, s, steps, d_rng, d_actions);
+  } else {
+    hipLaunchKernelGGL((k_env_rollout<MASK_SELECTED, false>), g, b, 0, st, s, steps, d_rng, d_actions);
+    hipLaunchKernelGGL((k_env_rollout<MASK_SELECTED, true>), g, b, 0, st, s, steps, d_rng, d_actions);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_seed_sampler(size_t n, uint32_t seed, uint32_t *d_rng, void *stream) {

@@ -2,13 +2,13 @@
 # build (here) or run (GPU box) the ablation variants of tools/ablate.cpp
 set -o pipefail
 if [ "$1" = build ]; then
-  for v in base STORES UPDOBS; do
+  for v in base STORES UPDOBS RESET; do
     f=""; [ $v != base ] && f="-DCOG_ABLATE_$v"
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off $f -Iinclude -Igym-eldorado_amd/csrc \
         tools/ablate.cpp -o tools/ablate_$v || exit 1
   done
   exit 0
 fi
-for v in base STORES UPDOBS; do
+for v in base STORES UPDOBS RESET; do
   printf "%-8s " $v; timeout -k 10 60 tools/ablate_$v 65536 3000 || exit 1
 done

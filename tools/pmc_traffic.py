@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 import pmc_summary  # noqa: E402
 
 # kernel -> (short name, steps per launch key)
-KERNELS = {"void cog::k_env_rollout<0>": "k_env_rollout", "void cog::k_env_step<0>": "k_env_step",
+KERNELS = {"void cog::k_env_rollout<0, false>": "k_env_rollout", "void cog::k_env_step<0>": "k_env_step",
            "void cog::k_encode_lds<true>": "k_encode"}
 
 
