@@ -1026,7 +1026,7 @@ struct RegEnv {
   uint32_t d[28];                                          // DeckObs of ag
   Heads sel, sta, stn;                                     // selected / stored(ag) / stored(na)
   bool moved;
-  uint4 g2;                                                // map bounds + locations (moves only)
+  uint4 g2;                                                // map bounds + locations
 
   DEV uint32_t n_players() const { return g1x & 0xffu; }
   DEV uint32_t done() const { return g1x >> 24; }
@@ -1266,6 +1266,16 @@ struct RegEnv {
 };
 
 // the mover's new neighbourhood (load_cells on registers + the compact code grid)
+// COG_DIRS_XY2 / 2 + 1 as 2-bit fields (direction d at bits 2d): no constant-memory load
+constexpr uint32_t dir_pack(int axis) {
+  const int8_t v[7][2] = COG_DIRS_XY2;
+  uint32_t r = 0;
+  for (int d = 0; d < 7; d++) r |= (uint32_t)(v[d][axis] / 2 + 1) << (2 * d);
+  return r;
+}
+DEV int dir_dx(int d) { return (int)((dir_pack(0) >> (2 * d)) & 3u) - 1; }
+DEV int dir_dy(int d) { return (int)((dir_pack(1) >> (2 * d)) & 3u) - 1; }
+
 DEV uint2 cells_at(const uint8_t *cgrid, const uint4 &g2, int lx, int ly) {
   const int minx = (int8_t)(g2.x & 0xffu), miny = (int8_t)((g2.x >> 8) & 0xffu);
   const int dimx = g2.y & 0xffu, dimy = (g2.y >> 8) & 0xffu;
@@ -1297,6 +1307,14 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
   float r0 = __uint_as_float(R.sh[1]), r1 = __uint_as_float(R.sh[2]), r2 = __uint_as_float(R.sh[3]);
   const int a_play = act[0], a_special = act[1], a_remove = act[2], a_move = act[3], a_shop = act[4];
   int special = COG_SPECIAL_NONE;
+  uint2 moved_cells = R.cells_a;
+  if (a_move && !a_play && !a_special) {                   // the destination's neighbourhood: its
+    const int lx = (int8_t)((R.g2.z >> (8 * ag)) & 0xffu) + dir_dx(a_move);   // loads are issued
+    const int ly = (int8_t)((R.g2.w >> (8 * ag)) & 0xffu) + dir_dy(a_move);   // first, used last
+    R.g2.z = (R.g2.z & ~(0xffu << (8 * ag))) | (((uint32_t)lx & 0xffu) << (8 * ag));
+    R.g2.w = (R.g2.w & ~(0xffu << (8 * ag))) | (((uint32_t)ly & 0xffu) << (8 * ag));
+    moved_cells = cells_at(s.cgrid + i * COG_CELLS, R.g2, lx, ly);
+  }
   if (a_play) {                                            // Player::play_card (player.cpp:45-60)
     const int c = a_play - 1;
     if (phase == COG_PHASE_MOVEMENT) {
@@ -1317,11 +1335,6 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
     special = (int)cardf(kSpecial, c);
   } else if (a_move) {                                     // move (environment.cpp:115-127)
     const uint32_t c = R.use_cell_dyn(R.cells_a, a_move);
-    R.g2 = reinterpret_cast<const uint4 *>(s.priv + i)[2]; // map bounds + locations
-    const int lx = (int8_t)((R.g2.z >> (8 * ag)) & 0xffu) + c_dirs[a_move][0] / 2;
-    const int ly = (int8_t)((R.g2.w >> (8 * ag)) & 0xffu) + c_dirs[a_move][1] / 2;
-    R.g2.z = (R.g2.z & ~(0xffu << (8 * ag))) | (((uint32_t)lx & 0xffu) << (8 * ag));
-    R.g2.w = (R.g2.w & ~(0xffu << (8 * ag))) | (((uint32_t)ly & 0xffu) << (8 * ag));
     if (!P.next_move_free) {                               // Player::handle_requirement (:141-162)
       const uint32_t req = COG_HEX_REQ(c), n = COG_HEX_N(c);
       if (req < 3) {
@@ -1419,8 +1432,7 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
   R.sh[0] = (R.sh[0] & ~0xffu) | phase;
   R.sh[1] = __float_as_uint(r0); R.sh[2] = __float_as_uint(r1); R.sh[3] = __float_as_uint(r2);
   if (R.moved) {                                           // the mover's new neighbourhood
-    R.cells_a = cells_at(s.cgrid + i * COG_CELLS, R.g2, (int8_t)((R.g2.z >> (8 * ag)) & 0xffu),
-                         (int8_t)((R.g2.w >> (8 * ag)) & 0xffu));
+    R.cells_a = moved_cells;
     if (na == ag) R.cells_n = R.cells_a;
   }
   PH(11);
@@ -1446,7 +1458,7 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
 // Snap: the step-start image of everything a step may modify; the store phase writes back the
 // 16-B granules that differ from it (and nothing else).
 struct Snap {
-  uint4 g0, g1;                       // EnvPriv granules 0, 1
+  uint4 g0, g1, g2;                   // EnvPriv granules 0, 1, 2
   uint32_t info_steps;                // EnvPriv granule 3, dword 0
   uint4 sh[3];                        // ObsData 16128..16175: phase, resources, shop
   MBits sel;                          // selected mask
@@ -1461,6 +1473,7 @@ DEV void load_env(const DevState &s, size_t i, Snap &S) {          // records at
   const uint4 *sh4 = reinterpret_cast<const uint4 *>(s.obs + i * COG_OBS_BYTES + COG_OBS_PHASE);
   S.g0 = pv4[0];
   S.g1 = pv4[1];
+  S.g2 = pv4[2];
   S.info_steps = reinterpret_cast<const uint32_t *>(pv4 + 3)[0];
   S.sel = mbits_of(s.heads[5 * i]);
   S.sh[0] = sh4[0];
@@ -1486,6 +1499,7 @@ DEV void regs_env(RegEnv &R, const Snap &S) {
   R.rng = S.g0.x; R.seed = S.g0.y; R.max_steps = S.g0.z; R.turn_counter = S.g0.w;
   R.g1x = S.g1.x; R.g1y = S.g1.y; R.in_market = S.g1.z; R.flags = S.g1.w;
   R.info_steps = S.info_steps;
+  R.g2 = S.g2;
   R.moved = false;
   R.sel = heads_of(S.sel);
 #pragma unroll
@@ -1770,6 +1784,7 @@ __global__ void __launch_bounds__(64) k_env_rollout(DevState s, int steps, uint3
       // the next step's image: registers (env level) and this wave's LDS (player level)
       S.g0 = make_uint4(R.rng, R.seed, R.max_steps, R.turn_counter);
       S.g1 = make_uint4(R.g1x, R.g1y, R.in_market, R.flags);
+      S.g2 = R.g2;
       S.info_steps = R.info_steps;
 #pragma unroll
       for (int k = 0; k < 3; k++) S.sh[k] = make_uint4(R.sh[4 * k], R.sh[4 * k + 1], R.sh[4 * k + 2], R.sh[4 * k + 3]);

@@ -1,5 +1,6 @@
 #!/bin/bash
-# build (here) or run (GPU box) the ablation variants of tools/ablate.cpp
+# build (here) or run (GPU box) the ablation variants of tools/ablate.cpp (build also makes
+# tools/stamp_step, the phase-stamp diagnostic)
 set -o pipefail
 if [ "$1" = build ]; then
   for v in base STORES UPDOBS RESET; do
@@ -7,6 +8,8 @@ if [ "$1" = build ]; then
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off $f -Iinclude -Igym-eldorado_amd/csrc \
         tools/ablate.cpp -o tools/ablate_$v || exit 1
   done
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DCOG_STAMPS -Iinclude \
+      -Igym-eldorado_amd/csrc tools/stamp_step.cpp -o tools/stamp_step || exit 1
   exit 0
 fi
 for v in base STORES UPDOBS RESET; do
