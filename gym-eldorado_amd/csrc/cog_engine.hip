@@ -1276,17 +1276,48 @@ constexpr uint32_t dir_pack(int axis) {
 DEV int dir_dx(int d) { return (int)((dir_pack(0) >> (2 * d)) & 3u) - 1; }
 DEV int dir_dy(int d) { return (int)((dir_pack(1) >> (2 * d)) & 3u) - 1; }
 
-DEV uint2 cells_at(const uint8_t *cgrid, const uint4 &g2, int lx, int ly) {
-  const int minx = (int8_t)(g2.x & 0xffu), miny = (int8_t)((g2.x >> 8) & 0xffu);
+// The 7 cells lie on 3 grid rows (x - 1 .. x + 1), 3 consecutive bytes each from column y - 1:
+// one 8-byte load per row from a dword-aligned start (48 is a multiple of 4, so every row has
+// the same alignment offset, <= 3, and the 3 bytes fit in the 8).  A start is clamped into the
+// env's grid, which only moves the windows of cells that are masked below anyway.
+// cell_rows issues the three loads; rows_ready takes all three windows at once through an empty
+// asm, so the loads stay back to back and in flight until the cells are needed (under register
+// pressure the scheduler otherwise serialises per-cell loads).  rows_ready runs in converged
+// control flow: the wait for the loads then sits on every path, and no later write of those
+// registers (the store phase reuses them) needs a conservative vmcnt(0) behind the stores.
+DEV int row_start(int ix, int iy0) { return min(max((ix * COG_GRID + iy0 - 1) & ~3, 0), COG_CELLS - 8); }
+struct CellRows {
+  uint32_t w[6];
+  int ix0, iy0;                                            // the centre in grid indices
+};
+DEV CellRows cell_rows(const uint8_t *cgrid, const uint4 &g2, int lx, int ly) {
+  CellRows c;
+  c.ix0 = lx - (int8_t)(g2.x & 0xffu) + 1;
+  c.iy0 = ly - (int8_t)((g2.x >> 8) & 0xffu) + 1;
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(cgrid + row_start(c.ix0 + r - 1, c.iy0));
+    c.w[2 * r] = p[0];
+    c.w[2 * r + 1] = p[1];
+  }
+  return c;
+}
+DEV void rows_ready(CellRows &c) {
+  asm volatile("" : "+v"(c.w[0]), "+v"(c.w[1]), "+v"(c.w[2]), "+v"(c.w[3]), "+v"(c.w[4]), "+v"(c.w[5]));
+}
+DEV uint2 cells_from_rows(const CellRows &c, const uint4 &g2) {
   const int dimx = g2.y & 0xffu, dimy = (g2.y >> 8) & 0xffu;
+  const int ix0 = c.ix0, iy0 = c.iy0;
+  const uint32_t *w = c.w;
   uint32_t v[7], oob = 0;
 #pragma unroll
   for (int dir = 0; dir < 7; dir++) {
-    const int ix = lx + c_dirs[dir][0] / 2 - minx + 1, iy = ly + c_dirs[dir][1] / 2 - miny + 1;
+    const int dx = dir_dx(dir), ix = ix0 + dx, iy = iy0 + dir_dy(dir);
     const bool out_ = ix < 0 || iy < 0 || ix >= dimx || iy >= dimy;
     const bool ring = ix >= COG_GRID || iy >= COG_GRID;
-    const int cx = min(max(ix, 0), COG_GRID - 1), cy = min(max(iy, 0), COG_GRID - 1);
-    const uint32_t c = cgrid[cx * COG_GRID + cy];
+    const uint64_t row = (uint64_t)w[2 * (dx + 1) + 1] << 32 | w[2 * (dx + 1)];
+    const int pos = ix * COG_GRID + iy - row_start(ix, iy0);   // 0..7 for every unmasked cell
+    const uint32_t c = (uint32_t)(row >> (8 * (pos & 7))) & 0xffu;
     v[dir] = (out_ || ring || !c) ? (uint32_t)COG_HEX_MOUNTAIN : c;
     oob |= (out_ ? 1u : 0u) << dir;
   }
@@ -1307,13 +1338,13 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
   float r0 = __uint_as_float(R.sh[1]), r1 = __uint_as_float(R.sh[2]), r2 = __uint_as_float(R.sh[3]);
   const int a_play = act[0], a_special = act[1], a_remove = act[2], a_move = act[3], a_shop = act[4];
   int special = COG_SPECIAL_NONE;
-  uint2 moved_cells = R.cells_a;
+  CellRows moved_rows = {};
   if (a_move && !a_play && !a_special) {                   // the destination's neighbourhood: its
     const int lx = (int8_t)((R.g2.z >> (8 * ag)) & 0xffu) + dir_dx(a_move);   // loads are issued
     const int ly = (int8_t)((R.g2.w >> (8 * ag)) & 0xffu) + dir_dy(a_move);   // first, used last
     R.g2.z = (R.g2.z & ~(0xffu << (8 * ag))) | (((uint32_t)lx & 0xffu) << (8 * ag));
     R.g2.w = (R.g2.w & ~(0xffu << (8 * ag))) | (((uint32_t)ly & 0xffu) << (8 * ag));
-    moved_cells = cells_at(s.cgrid + i * COG_CELLS, R.g2, lx, ly);
+    moved_rows = cell_rows(s.cgrid + i * COG_CELLS, R.g2, lx, ly);
   }
   if (a_play) {                                            // Player::play_card (player.cpp:45-60)
     const int c = a_play - 1;
@@ -1431,8 +1462,9 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
   }
   R.sh[0] = (R.sh[0] & ~0xffu) | phase;
   R.sh[1] = __float_as_uint(r0); R.sh[2] = __float_as_uint(r1); R.sh[3] = __float_as_uint(r2);
+  rows_ready(moved_rows);
   if (R.moved) {                                           // the mover's new neighbourhood
-    R.cells_a = moved_cells;
+    R.cells_a = cells_from_rows(moved_rows, R.g2);
     if (na == ag) R.cells_n = R.cells_a;
   }
   PH(11);
