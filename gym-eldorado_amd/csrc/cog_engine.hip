@@ -1115,24 +1115,44 @@ struct RegEnv {
 #pragma unroll
     for (int q = 0; q < 5; q++) total = sum8(d[q], total);
     if (total == P.n_in_draw && total < 128u) {            // every prefix sum fits in 7 bits
+      uint32_t dm = 0;                                     // types drawn
       for (uint32_t i = 0; i < n; i++) {
-        const uint32_t T = bcast8(uid_fast(rng, P.n_in_draw) + 1u);
+        const uint32_t k = P.n_in_draw;                    // piles of <= 31: division-free draw
+        const uint32_t T = bcast8((k <= 31u ? uid_small(rng, k) : uid_fast(rng, k)) + 1u);
         uint32_t c = 0;
 #pragma unroll
         for (int q = 0; q < 6; q++)                        // bytes with prefix <= t: bit 7 clear
           c += __popc(~((pre[q] | 0x80808080u) - T) & (q < 5 ? 0x80808080u : 0x80u));
-        const int qc = (int)(c >> 2);
-        const uint32_t sh = 8u * (c & 3u);
 #pragma unroll
-        for (int q = 0; q < 6; q++) {
-          pre[q] -= q > qc ? 0x01010101u : (q == qc ? 0x01010101u << sh : 0u);
-          d[q] -= q == qc ? 1u << sh : 0u;                 // draw[c] >= 1: no borrow
+        for (int q = 0; q < 6; q++) {                      // prefix sums of types >= c drop by one
+          const int s8 = min(max(8 * ((int)c - 4 * q), 0), 32);   // (>= 1 there: no borrow)
+          pre[q] -= s8 >= 32 ? 0u : 0x01010101u << s8;
         }
-        P.n_in_draw = (P.n_in_draw - 1) & 0xffu;
-        pile_add<COG_DECK_HAND>(d, (int)c, 1u);
-        sel.play |= 1u << (c + 1);
-        sel.spec = set_bit(sel.spec, (int)c + 1, is_special((int)c));
+        P.n_in_draw = (k - 1u) & 0xffu;
+        dm |= 1u << c;
       }
+      // the pile back from its prefix sums (nondecreasing bytes < 128: no borrows), and the drawn
+      // counts (old pile - new pile, no borrows either) added to the hand: byte k of the draw
+      // pile's dword grid is hand byte 21 + k.  The selected mask gains the drawn types (its
+      // play_special bits only ever hold special types, so setting is all the reference's
+      // per-card assignment does).
+      uint32_t h[6], prevp = 0;
+#pragma unroll
+      for (int q = 0; q < 6; q++) {
+        const uint32_t nd = pre[q] - fsh8(pre[q], prevp, 3);   // p[k] - p[k-1]
+        prevp = pre[q];
+        if (q < 5) {
+          h[q] = d[q] - nd;
+          d[q] = nd;
+        } else {
+          h[5] = (d[5] - nd) & 0xffu;
+          d[5] = (d[5] & 0xffffff00u) | (nd & 0xffu);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 6; q++) d[5 + q] = add8(d[5 + q], fsh8(h[q], q ? h[q - 1] : 0u, 3));
+      sel.play |= dm << 1;
+      sel.spec |= (dm & kSpecialBits) << 1;
     } else {
       for (uint32_t i = 0; i < n; i++) {
         const uint32_t t = uid_fast(rng, P.n_in_draw);
