@@ -20,8 +20,22 @@ environment without a usable device raises RuntimeError.
 """
 from __future__ import annotations
 
+import os
 import sys
 import types
+
+# torch (ROCm) and this engine load the same HIP runtime (SONAME libamdhip64.so.7).  torch rejects
+# a runtime another library has already brought up ("No HIP GPUs are available"), while the
+# engine is happy with torch's, so when torch is installed its GPU side is brought up first.
+# COG_NO_TORCH=1 skips this (torch interop, e.g. device_tensors, then needs torch initialised
+# before the first environment is created).
+if not os.environ.get("COG_NO_TORCH"):
+    try:
+        import torch as _torch
+        if _torch.cuda.is_available():
+            _torch.cuda.init()
+    except Exception:
+        pass
 
 from . import _city_of_gold as _C
 
@@ -91,6 +105,22 @@ def _getter(module, prefix, factory):
     return get
 
 
+DEVICE_VIEWS = ("observations", "selected_action_masks", "rewards", "dones", "agent_selection", "infos")
+
+
+def device_tensors(env, sampler=None):
+    """The env's device views (and the sampler's device actions) as torch tensors, zero copy via
+    DLPack: rows are records, as uint8 bytes (rewards: float32 (N, 4)); they alias the engine
+    state, which the engine updates on its own HIP stream (`env.stream()`), so synchronise
+    (runner.sync() / env.sync_host()) before reading.  The reference's docs suggest TensorDict
+    over copies of the numpy views (docs/source/index.rst:20-26); these need no copy."""
+    import torch
+    out = {nm: torch.from_dlpack(env.dlpack(nm)) for nm in DEVICE_VIEWS}
+    if sampler is not None:
+        out["actions"] = torch.from_dlpack(sampler.dlpack())
+    return out
+
+
 get_vec_env = _getter(vec.sampler, VEC_ENV_CLS, _make_env_cls)
 get_vec_sampler = _getter(vec.env, VEC_SAMPLER_CLS, _make_sampler_cls)
 get_runner = _getter(vec.runner, VEC_RUNNER_CLS, _make_runner_cls)
@@ -102,4 +132,4 @@ for _n in list(range(0, 9)) + [16, 32, 64, 128, 256]:
 del _n, _m
 
 __all__ = ["vec", "Difficulty", "EASY", "MEDIUM", "HARD", "ObsData", "ActionMask", "ActionData", "Info",
-           "DeckObs", "get_vec_env", "get_vec_sampler", "get_runner", "device_count"]
+           "DeckObs", "get_vec_env", "get_vec_sampler", "get_runner", "device_count", "device_tensors"]

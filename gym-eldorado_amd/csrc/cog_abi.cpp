@@ -421,6 +421,7 @@ int cog_env_time_encode(cog_env *env, int iters, int variant, double *ms_per_lau
 
 void *cog_env_stream(cog_env *env) { return env ? (void *)env->stream : nullptr; }
 int cog_env_device(const cog_env *env) { return env ? env->device : -1; }
+int cog_sampler_device(const cog_sampler *s) { return s ? s->device : -1; }
 
 // ---- sampler -----------------------------------------------------------------------------
 int cog_sampler_create(size_t n_envs, uint64_t seed, int device, cog_sampler **out) {

@@ -102,6 +102,71 @@ static const T *checked_records(const py::array &a, size_t n, const char *what) 
   return static_cast<const T *>(a.data());
 }
 
+// ---- DLPack export of the device views (zero-copy device consumers) ------
+// The DLPack v0.x C structs (dlpack.h ABI), declared here rather than pulled from a framework.
+struct DLDevice {
+  int32_t device_type, device_id;
+};
+struct DLDataType {
+  uint8_t code, bits;
+  uint16_t lanes;
+};
+struct DLTensor {
+  void *data;
+  DLDevice device;
+  int32_t ndim;
+  DLDataType dtype;
+  int64_t *shape, *strides;
+  uint64_t byte_offset;
+};
+struct DLManagedTensor {
+  DLTensor dl_tensor;
+  void *manager_ctx;
+  void (*deleter)(DLManagedTensor *self);
+};
+constexpr int32_t kDLROCM = 10;
+constexpr uint8_t kDLUInt = 1, kDLFloat = 2;
+
+struct DLHolder {                     // owns the shape array and a reference to the owning object
+  DLManagedTensor t;
+  int64_t shape[2];
+  PyObject *owner;
+};
+static void dl_delete(DLManagedTensor *self) {
+  DLHolder *h = reinterpret_cast<DLHolder *>(self->manager_ctx);
+  {
+    py::gil_scoped_acquire g;
+    Py_XDECREF(h->owner);
+  }
+  delete h;
+}
+// a "dltensor" capsule over n records of `width` elements of (code, bits) at device address p
+// (width 0: a 1-D tensor of n elements); the consumer's tensor keeps `owner` alive
+static py::capsule dl_capsule(void *p, int device, size_t n, int64_t width, uint8_t code, uint8_t bits, py::handle owner) {
+  DLHolder *h = new DLHolder();
+  h->shape[0] = (int64_t)n;
+  h->shape[1] = width;
+  h->owner = owner.ptr();
+  Py_XINCREF(h->owner);
+  DLTensor &t = h->t.dl_tensor;
+  t.data = p;
+  t.device = DLDevice{kDLROCM, device};
+  t.ndim = width > 0 ? 2 : 1;
+  t.dtype = DLDataType{code, bits, 1};
+  t.shape = h->shape;
+  t.strides = nullptr;                // compact row-major
+  t.byte_offset = 0;
+  h->t.manager_ctx = h;
+  h->t.deleter = dl_delete;
+  return py::capsule(&h->t, "dltensor", [](PyObject *cap) {
+    // only an unconsumed capsule still owns its tensor (consumers rename it "used_dltensor")
+    if (PyCapsule_IsValid(cap, "dltensor")) {
+      auto *m = static_cast<DLManagedTensor *>(PyCapsule_GetPointer(cap, "dltensor"));
+      if (m && m->deleter) m->deleter(m);
+    }
+  });
+}
+
 // ---- vec env (py_vec_env, vectorized.h:25-105) -------------------------------------------
 class VecEnv {
  public:
@@ -264,6 +329,25 @@ PYBIND11_MODULE(_city_of_gold, m) {
                         "rewards"_a = (uintptr_t)v.d_rewards, "dones"_a = (uintptr_t)v.d_dones,
                         "agent_selection"_a = (uintptr_t)v.d_agent_selection, "infos"_a = (uintptr_t)v.d_infos);
       })
+      .def("dlpack", [](py::object self, const std::string &name) {
+        // one device view as a DLPack capsule (torch.from_dlpack, TensorDict); rows are records
+        VecEnv &e = self.cast<VecEnv &>();
+        auto v = e.views();
+        const int dev = cog_env_device(e.handle());
+        const size_t n = v.n_envs;
+        if (name == "observations") return dl_capsule(v.d_observations, dev, n, sizeof(ObsData), kDLUInt, 8, self);
+        if (name == "selected_action_masks")
+          return dl_capsule(v.d_selected_action_masks, dev, n, sizeof(ActionMask), kDLUInt, 8, self);
+        if (name == "rewards") return dl_capsule(v.d_rewards, dev, n, 4, kDLFloat, 32, self);
+        if (name == "dones") return dl_capsule(v.d_dones, dev, n, 0, kDLUInt, 8, self);
+        if (name == "agent_selection") return dl_capsule(v.d_agent_selection, dev, n, 0, kDLUInt, 8, self);
+        if (name == "infos") return dl_capsule(v.d_infos, dev, n, sizeof(Info), kDLUInt, 8, self);
+        throw py::value_error("no device view named " + name);
+      }, "name"_a)
+      .def("step_device", [](VecEnv &e, uintptr_t d_actions) {
+        // step with ActionData records already in device memory (e.g. a torch tensor's data_ptr())
+        check(cog_env_step_device(e.handle(), reinterpret_cast<const void *>(d_actions), e.num_envs()));
+      }, "d_actions"_a)
       .def("stream", [](VecEnv &e) { return (uintptr_t)cog_env_stream(e.handle()); })
       .def("hazards", [](VecEnv &e) {
         py::array_t<uint32_t> per((py::ssize_t)e.num_envs());
@@ -287,7 +371,12 @@ PYBIND11_MODULE(_city_of_gold, m) {
         return view(s.actions(), s.num_envs(), self);
       })
       .def("sample", &VecSampler::sample, "action_mask"_a)
-      .def("device_actions", [](VecSampler &s) { return (uintptr_t)cog_sampler_device_actions(s.handle()); });
+      .def("device_actions", [](VecSampler &s) { return (uintptr_t)cog_sampler_device_actions(s.handle()); })
+      .def("dlpack", [](py::object self) {       // the device actions (ActionData rows)
+        VecSampler &s = self.cast<VecSampler &>();
+        return dl_capsule(cog_sampler_device_actions(s.handle()), cog_sampler_device(s.handle()), s.num_envs(),
+                          sizeof(ActionData), kDLUInt, 8, self);
+      });
 
   py::class_<Runner>(m, "RunnerBase", py::dynamic_attr())
       .def(py::init<VecEnv &, VecSampler &, std::optional<size_t>, bool, bool>(), "env"_a, "sampler"_a,

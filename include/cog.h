@@ -136,6 +136,7 @@ COG_API int cog_sampler_sample(cog_sampler *s, const cog_action_mask_t *masks, s
 COG_API int cog_sampler_sample_device(cog_sampler *s, const void *d_masks, size_t n);
 COG_API cog_action_t *cog_sampler_actions(cog_sampler *s);   /* persistent host view */
 COG_API void *cog_sampler_device_actions(cog_sampler *s);    /* device view */
+COG_API int cog_sampler_device(const cog_sampler *s);       /* device ordinal */
 
 /* ---- runner: asynchronous sample/step on the env's stream (runner.h:81-100) ----------------- */
 COG_API int cog_runner_create(cog_env *env, cog_sampler *s, size_t n_threads, uint32_t flags,
