@@ -86,3 +86,36 @@ def test_rollout_interleaves_with_host_steps(cg):
         orc.step(osm.actions)
     for nm in ("observations", "selected_action_masks", "infos"):
         assert po.named_equal(getattr(env, nm), getattr(orc, nm)) is None, nm
+
+
+@pytest.mark.parametrize("n,chunk", [(1, 7), (100, 33), (130, 1000)])
+def test_rollout_ragged_batches_against_oracle(cg, n, chunk):
+    """Batches that leave the last wave partly empty (and a chunk larger than the run), with
+    episodes short enough that lanes park and resume inside one launch."""
+    steps = 150
+    env, smp, _ = run(cg, n, 2024 + n, 4, 2, 30, steps, chunk, True)
+    orc, osm = po.OracleVec(n), po.OracleSampler(n, 2024 + n)
+    orc.reset(2024 + n, 4, 3, 2, 30)
+    for _ in range(steps):
+        osm.sample(po.stored_masks(orc))
+        orc.step(osm.actions)
+    for nm in ("observations", "selected_action_masks", "infos"):
+        assert po.named_equal(getattr(env, nm), getattr(orc, nm)) is None, nm
+    assert np.array_equal(env.rewards, orc.rewards)
+    assert np.array_equal(env.dones, orc.dones)
+    assert np.array_equal(env.agent_selection, orc.agent_selection)
+
+
+def test_rollout_zero_steps_and_empty_batch(cg):
+    env, smp, runner = run(cg, 64, 5, 4, 2, 100000, 0, 10, False)   # rollout(0): nothing runs
+    before = env.observations.copy()
+    runner.rollout(0)
+    runner.sync()
+    env.sync_host()
+    assert po.named_equal(env.observations, before) is None
+    e0 = cg.vec.get_vec_env(0)()
+    s0 = cg.vec.get_vec_sampler(0)(1)
+    r0 = cg.vec.get_runner(0)(e0, s0, None, device_views=True)
+    r0.set_chunk(8)
+    r0.rollout(20)
+    r0.sync()
