@@ -121,6 +121,8 @@ def device_tensors(env, sampler=None):
     return out
 
 
+from .single import cog_env  # noqa: E402  (src/pybind/single_env.cpp: the single-env API)
+
 get_vec_env = _getter(vec.sampler, VEC_ENV_CLS, _make_env_cls)
 get_vec_sampler = _getter(vec.env, VEC_SAMPLER_CLS, _make_sampler_cls)
 get_runner = _getter(vec.runner, VEC_RUNNER_CLS, _make_runner_cls)
@@ -132,4 +134,4 @@ for _n in list(range(0, 9)) + [16, 32, 64, 128, 256]:
 del _n, _m
 
 __all__ = ["vec", "Difficulty", "EASY", "MEDIUM", "HARD", "ObsData", "ActionMask", "ActionData", "Info",
-           "DeckObs", "get_vec_env", "get_vec_sampler", "get_runner", "device_count", "device_tensors"]
+           "DeckObs", "get_vec_env", "get_vec_sampler", "get_runner", "device_count", "device_tensors", "cog_env"]

@@ -247,6 +247,7 @@ int cog_env_create(size_t n_envs, int device, cog_env **out) {
   s.n = n;
   s.first = 0;
   s.cap = n;
+  s.autoreset = 1;
   if ((rc = dmalloc(&s.obs, n * COG_OBS_BYTES)) || (rc = dmalloc(&s.sel, n * COG_MASK_BYTES)) ||
       (rc = dmalloc(&s.info, n * COG_INFO_BYTES)) || (rc = dmalloc(&s.rew, n * 4 * sizeof(float))) ||
       (rc = dmalloc(&s.done, n)) || (rc = dmalloc(&s.agent, n)) ||
@@ -421,6 +422,13 @@ int cog_env_time_encode(cog_env *env, int iters, int variant, double *ms_per_lau
 
 void *cog_env_stream(cog_env *env) { return env ? (void *)env->stream : nullptr; }
 int cog_env_device(const cog_env *env) { return env ? env->device : -1; }
+int cog_env_set_autoreset(cog_env *env, int on) {
+  if (!env) return fail(COG_ERR_INVALID, "env is NULL");
+  DeviceGuard g(env->device);
+  if (hipStreamSynchronize(env->stream) != hipSuccess) return fail(COG_ERR_HIP, "hipStreamSynchronize failed");
+  env->s.autoreset = on ? 1u : 0u;
+  return COG_OK;
+}
 int cog_sampler_device(const cog_sampler *s) { return s ? s->device : -1; }
 
 // ---- sampler -----------------------------------------------------------------------------

@@ -99,6 +99,8 @@ struct DevState {
   uint32_t *park;                    // [n] rollout hand-over: step of a pending episode end, or ~0
   size_t first;                      // global index of env 0 (sub-range launches; dirty list ids)
   size_t cap;                        // capacity of the dirty list
+  uint32_t autoreset;                // 1: vec_cog_env (reset a finished env in the same call,
+                                     // vec_environment.h:56-59); 0: cog_env (stays done)
   unsigned long long *stamps;        // diagnostic builds (COG_STAMPS) only: per-wave phase clocks
 };
 

@@ -1650,7 +1650,7 @@ DEV bool end_of_step(const DevState &s, size_t i, bool was_done, bool finish, ui
   const bool done = was_done || finish;
   if ((out & 0xffu) != (done ? 1u : 0u)) s.done[i] = done ? 1 : 0;   // dones[i] before the auto-reset
   bool enc = false;
-  if (done) {
+  if (done && s.autoreset) {
     Ctx e = make_ctx(s, i);
     if (!env_reset(e)) {
       atomicOr(&s.status[0], e.pv->flags);

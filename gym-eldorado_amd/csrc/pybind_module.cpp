@@ -348,6 +348,7 @@ PYBIND11_MODULE(_city_of_gold, m) {
         // step with ActionData records already in device memory (e.g. a torch tensor's data_ptr())
         check(cog_env_step_device(e.handle(), reinterpret_cast<const void *>(d_actions), e.num_envs()));
       }, "d_actions"_a)
+      .def("set_autoreset", [](VecEnv &e, bool on) { check(cog_env_set_autoreset(e.handle(), on ? 1 : 0)); }, "on"_a)
       .def("stream", [](VecEnv &e) { return (uintptr_t)cog_env_stream(e.handle()); })
       .def("hazards", [](VecEnv &e) {
         py::array_t<uint32_t> per((py::ssize_t)e.num_envs());

@@ -124,6 +124,10 @@ COG_API void *cog_env_stream(cog_env *env);     /* hipStream_t of the handle */
  * variant: 0 = production kernel, >0 = alternative implementations kept for A/B timing. */
 COG_API int cog_env_time_encode(cog_env *env, int iters, int variant, double *ms_per_launch);
 COG_API int cog_env_device(const cog_env *env); /* device ordinal */
+/* on (default): a finished env is reset inside the same step call, as vec_cog_env<N>::step does
+ * (vec_environment.h:56-59).  off: cog_env::step semantics (environment.cpp:91-95) -- the env
+ * stays done and later steps are dead steps until reset() */
+COG_API int cog_env_set_autoreset(cog_env *env, int on);
 
 /* ---- masked uniform random sampler ------------------------------------------------------- */
 /* vec_action_sampler<N>(seed) (vec_sampler.h:9-13): sampler i seeded seed + i (no u32 wrap). */
