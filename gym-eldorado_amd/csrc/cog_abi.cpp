@@ -108,12 +108,6 @@ struct cog_runner {
   std::vector<hipEvent_t> ev;         // pairs: one per step() launch or one per rollout() batch
   size_t ev_used = 0;
   uint64_t timed_launches = 0;        // fused launches covered by the recorded pairs
-  // rollout lanes: the batch split into contiguous env blocks, each stepped on a stream of its
-  // own (the reference runner's per-thread env blocks, runner.h:36-38), forked from and joined
-  // back into the env's stream around every rollout
-  std::vector<hipStream_t> lanes;
-  std::vector<hipEvent_t> lane_ev;    // [0] fork, [1 + k] join of lane k
-  uint32_t stagger_ns = 0;
   int chunk = 1;                      // rollout steps per launch (>1: persistent K-step kernel)
 };
 
@@ -502,31 +496,8 @@ int cog_runner_create(cog_env *env, cog_sampler *s, size_t n_threads, uint32_t f
   r->smp = s;
   r->n_threads = n_threads;
   r->flags = flags;
-  const char *lv = std::getenv("COG_RUNNER_LANES");        // experiment knob (A/B of lane counts)
-  const int n_lanes = lv ? std::atoi(lv) : 1;
-  const char *cv = std::getenv("COG_RUNNER_CHUNK");
+  const char *cv = std::getenv("COG_RUNNER_CHUNK");        // default rollout steps per launch
   r->chunk = cv ? std::max(1, std::atoi(cv)) : 1;
-  const char *sv = std::getenv("COG_RUNNER_STAGGER_NS");
-  r->stagger_ns = sv ? (uint32_t)std::atoi(sv) : 0u;
-  if (n_lanes > 1 && env->s.n >= (size_t)n_lanes * 64) {
-    DeviceGuard g(env->device);
-    for (int k = 0; k < n_lanes; k++) {
-      hipStream_t st;
-      if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
-        cog_runner_destroy(r);
-        return fail(COG_ERR_HIP, "hipStreamCreate failed");
-      }
-      r->lanes.push_back(st);
-    }
-    for (int k = 0; k <= n_lanes; k++) {
-      hipEvent_t ev;
-      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
-        cog_runner_destroy(r);
-        return fail(COG_ERR_HIP, "hipEventCreate failed");
-      }
-      r->lane_ev.push_back(ev);
-    }
-  }
   *out = r;
   return COG_OK;
 }
@@ -535,10 +506,7 @@ void cog_runner_destroy(cog_runner *r) {
   if (!r) return;
   DeviceGuard g(r->env->device);
   (void)hipStreamSynchronize(r->env->stream);
-  for (hipStream_t st : r->lanes) (void)hipStreamSynchronize(st);
   for (hipEvent_t ev : r->ev) (void)hipEventDestroy(ev);
-  for (hipEvent_t ev : r->lane_ev) (void)hipEventDestroy(ev);
-  for (hipStream_t st : r->lanes) (void)hipStreamDestroy(st);
   delete r;
 }
 
@@ -547,12 +515,9 @@ size_t cog_runner_n_threads(const cog_runner *r) { return r ? r->n_threads : 0; 
 static int runner_flush_sample(cog_runner *r) {
   if (!r->pending_sample) return COG_OK;
   r->pending_sample = false;
-  const uint8_t *masks = r->env->s.sel;
-  if (r->flags & COG_RUNNER_STORED_MASKS) {
-    // stored-mask sampling exists only fused with a step; a lone sample reads the selected masks
-    // of the reference runner (runner.h:26,48)
-  }
-  return sampler_run(r->smp, masks, r->env->stream, false);
+  // a lone sample reads the selected masks, as the reference runner's does (runner.h:26,48);
+  // stored-mask sampling exists only fused with a step
+  return sampler_run(r->smp, r->env->s.sel, r->env->stream, false);
 }
 
 static int runner_timing_event(cog_runner *r, hipEvent_t *out) {
@@ -574,36 +539,15 @@ static int runner_launch_fused(cog_runner *r, int steps) {
   int rc;
   if (r->timing && (rc = runner_timing_event(r, &ev))) return rc;
   const int src = (r->flags & COG_RUNNER_STORED_MASKS) ? cog::MASK_STORED : cog::MASK_SELECTED;
-  const size_t L = r->lanes.size();
   if (r->chunk > 1) {                                      // persistent kernels, chunk steps each
     for (int t = 0; t < steps; t += r->chunk)
       if (cog::launch_rollout(r->env->s, src, std::min(r->chunk, steps - t), r->smp->d_rng, r->smp->d_actions,
                               r->env->stream))
         return fail(COG_ERR_HIP, std::string("rollout launch failed: ") + hipGetErrorString(hipGetLastError()));
-  } else if (L == 0) {
+  } else {
     for (int t = 0; t < steps; t++)
       if (cog::launch_sample_step(r->env->s, src, r->smp->d_rng, r->smp->d_actions, r->env->stream))
         return fail(COG_ERR_HIP, std::string("sample_step launch failed: ") + hipGetErrorString(hipGetLastError()));
-  } else {
-    // fork: every lane waits for the work already on the env's stream
-    HIPCHK(hipEventRecord(r->lane_ev[0], r->env->stream));
-    const size_t n = r->env->s.n, blk = (n / L + 63) / 64 * 64;
-    for (size_t k = 0; k < L; k++) {
-      HIPCHK(hipStreamWaitEvent(r->lanes[k], r->lane_ev[0], 0));
-      if (r->stagger_ns && k) cog::launch_spin(r->stagger_ns * (uint32_t)k, r->lanes[k]);
-    }
-    for (int t = 0; t < steps; t++)
-      for (size_t k = 0; k < L; k++) {
-        const size_t lo = std::min(n, k * blk), hi = k + 1 == L ? n : std::min(n, (k + 1) * blk);
-        if (lo >= hi) continue;
-        if (cog::launch_sample_step(cog::sub_state(r->env->s, lo, hi), src, r->smp->d_rng + lo,
-                                    r->smp->d_actions + lo * COG_ACTION_BYTES, r->lanes[k]))
-          return fail(COG_ERR_HIP, std::string("sample_step launch failed: ") + hipGetErrorString(hipGetLastError()));
-      }
-    for (size_t k = 0; k < L; k++) {                       // join
-      HIPCHK(hipEventRecord(r->lane_ev[1 + k], r->lanes[k]));
-      HIPCHK(hipStreamWaitEvent(r->env->stream, r->lane_ev[1 + k], 0));
-    }
   }
   if (r->timing) {
     if ((rc = runner_timing_event(r, &ev))) return rc;

@@ -145,6 +145,5 @@ int launch_sample_step(const DevState &s, int mask_source, uint32_t *d_rng, uint
 int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions,
                    void *stream);                    // persistent K-step runner loop
 int launch_seed_sampler(size_t n, uint32_t seed, uint32_t *d_rng, void *stream);
-int launch_spin(uint32_t ns, void *stream);         // a one-wave kernel that waits ~ns (stream stagger)
 
 }  // namespace cog

@@ -1894,11 +1894,6 @@ __global__ void k_sync_heads(DevState s) {
   if (i < s.n) sync_heads(s, i);
 }
 
-__global__ void k_spin(uint32_t ns) {                      // wall clock: 100 MHz s_memrealtime
-  const uint64_t t0 = wall_clock64(), ticks = ns / 10u;
-  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
-}
-
 __global__ void k_seed_sampler(size_t n, uint32_t seed, uint32_t *rngs) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) rngs[i] = mr_seed((uint64_t)seed + (uint64_t)i);   // vec_sampler.h:9-13 (no u32 wrap)
@@ -1951,10 +1946,6 @@ int launch_sample_step(const DevState &s, int mask_source, uint32_t *d_rng, uint
   else
     hipLaunchKernelGGL(k_env_step<MASK_SELECTED>, dim3(blocks_for(s.n, 64)), dim3(64), 0, (hipStream_t)stream, s,
                        nullptr, d_rng, d_actions);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-int launch_spin(uint32_t ns, void *stream) {
-  hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, (hipStream_t)stream, ns);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions, void *stream) {
