@@ -882,12 +882,37 @@ DEV uint8_t pick(uint32_t &rng, uint32_t m) {
   }
   return (uint8_t)nth_set_bit(m, uid_small(rng, k));      // k <= 22: division-free
 }
+// The five heads draw in order, one accepted draw per non-empty head.  Every head has <= 22
+// candidates, so a draw below kSmallSafe is accepted whatever k is: the draws are taken
+// branch-free first (the state advances past a head only if it has candidates), and only the
+// heads with two or more candidates do arithmetic.  A lane holding a draw that might be rejected
+// (probability < 2^-25 per head) redoes the sampling the sequential way, rejections included.
 DEV void sample_heads(const Heads &h, uint32_t &rng, uint8_t out[5]) {
-  out[0] = pick(rng, h.play);
-  out[1] = pick(rng, h.spec);
-  out[2] = pick(rng, h.rem);
-  out[3] = pick(rng, h.move);
-  out[4] = pick(rng, h.shop);
+  const uint32_t m[5] = {h.play, h.spec, h.rem, h.move, h.shop};
+  uint32_t x = rng, r[5], k[5];
+  bool risk = false;
+#pragma unroll
+  for (int j = 0; j < 5; j++) {
+    k[j] = __popc(m[j]);
+    uint32_t xn = x;
+    r[j] = mr_next(xn) - 1u;
+    x = k[j] ? xn : x;
+    risk |= k[j] != 0u && r[j] >= kSmallSafe;
+  }
+  if (risk) {
+    uint32_t y = rng;
+#pragma unroll
+    for (int j = 0; j < 5; j++) out[j] = pick(y, m[j]);
+    rng = y;
+    return;
+  }
+  rng = x;
+#pragma unroll
+  for (int j = 0; j < 5; j++) {
+    uint32_t v = k[j] ? (uint32_t)(__ffs(m[j]) - 1) : 0u;
+    if (k[j] >= 2u) v = nth_set_bit(m[j], uid_small_accepted(r[j], k[j]));
+    out[j] = (uint8_t)v;
+  }
 }
 DEV void sample_mask(const uint8_t *mask, uint32_t &rng, uint8_t out[5]) {
   sample_heads(heads_of(mbits_from_bytes(mask)), rng, out);
@@ -1821,6 +1846,14 @@ __global__ void __launch_bounds__(64) k_env_rollout(DevState s, int steps, uint3
       uint8_t act[5];
       PH(0);
       if (SRC == MASK_SELECTED) step_action<SRC>(R, nullptr, i, srng, act);
+#ifdef COG_ABLATE_DUPSAMPLE                                // diagnostic timing builds only: the
+      {                                                    // sampler's cost, measured by running
+        uint32_t r2 = srng ^ 0x5555u;                      // it a second time on a discarded state
+        uint8_t a2[5];
+        sample_heads(R.sel, r2, a2);
+        asm volatile("" ::"v"((uint32_t)a2[0] | a2[1] << 8 | a2[2] << 16 | (uint32_t)a2[3] << 24), "v"(a2[4] ^ r2));
+      }
+#endif
       regs_players(R, S);
       if (SRC == MASK_STORED) step_action<SRC>(R, nullptr, i, srng, act);
       store_action(actions_out + i * COG_ACTION_BYTES, act);

@@ -68,16 +68,24 @@ constexpr uint64_t residues5(uint32_t k0) {                // 12 residues of 5 b
   return v;
 }
 constexpr uint64_t kRes5_1 = residues5(1), kRes5_13 = residues5(13), kRes5_25 = residues5(25);
-COG_HD uint32_t uid_small(uint32_t &x, uint32_t k) {       // k in [1, 31]
+COG_HD uint32_t small_past(uint32_t k) {                  // k * (range / k), k in [1, 31]
   const uint64_t tab = k < 13 ? kRes5_1 : (k < 25 ? kRes5_13 : kRes5_25);
   const uint32_t j = k < 13 ? k - 1u : (k < 25 ? k - 13u : k - 25u);
-  const uint32_t m = (uint32_t)(tab >> (5u * j)) & 31u;
-  const uint32_t past = kUrngRange - m;
-  uint32_t r = mr_next(x) - 1u;
-  while (r >= past) r = mr_next(x) - 1u;
+  return kUrngRange - ((uint32_t)(tab >> (5u * j)) & 31u);
+}
+COG_HD uint32_t uid_small_accepted(uint32_t r, uint32_t k) {   // r < small_past(k): the value
+  const uint32_t past = small_past(k);
   const uint64_t rk = (uint64_t)r * k;
   const uint32_t q = div_range(rk);
   return q + ((uint64_t)(q + 1u) * past <= rk ? 1u : 0u);
 }
+COG_HD uint32_t uid_small(uint32_t &x, uint32_t k) {       // k in [1, 31]
+  const uint32_t past = small_past(k);
+  uint32_t r = mr_next(x) - 1u;
+  while (r >= past) r = mr_next(x) - 1u;
+  return uid_small_accepted(r, k);
+}
+// every draw a k in [1, 31] can reject has r >= range - 30 (range mod k <= 30)
+constexpr uint32_t kSmallSafe = kUrngRange - 31u;
 
 }  // namespace cog

@@ -67,3 +67,25 @@ def test_rollout_parity(cg, mode):
         env.step(smp.get_actions())
         orc.step(osm.actions)
         assert_same(env, orc, f"{mode} step {t}")
+
+
+def test_sampler_draws_at_the_rejection_boundary(cg):
+    """Sampler states whose j-th draw lands within 31 of the top of the range, where a head's
+    draw may be rejected: the engine's sequential fallback path against the oracle."""
+    P, RANGE = 2 ** 31 - 1, 2147483645
+    inv = pow(16807, -1, P)
+    rng = np.random.default_rng(11)
+    raw = np.zeros((1, 128), dtype=np.uint8)
+    raw[0, :92] = rng.random(92) < 0.5
+    raw[0, [0, 22, 44, 66, 73]] = 1                       # every head has candidates
+    masks = raw.view(po.MASK).reshape(1)
+    for j in (0, 1, 4):                                  # which draw hits the boundary
+        for r in range(RANGE - 34, RANGE + 1):
+            x = (r + 1) * inv % P                        # state before the draw giving r
+            for _ in range(j):
+                x = x * inv % P                          # ... j draws earlier
+            s, o = cg.vec.get_vec_sampler(1)(x), po.OracleSampler(1, x)
+            for _ in range(2):
+                s.sample(masks)
+                o.sample(masks)
+                assert po.named_equal(s.get_actions(), o.actions) is None, (j, r)
