@@ -1507,7 +1507,9 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
   }
   R.sh[0] = (R.sh[0] & ~0xffu) | phase;
   R.sh[1] = __float_as_uint(r0); R.sh[2] = __float_as_uint(r1); R.sh[3] = __float_as_uint(r2);
+#ifndef COG_ABLATE_ROWS                                    // diagnostic timing builds only
   rows_ready(moved_rows);
+#endif
   if (R.moved) {                                           // the mover's new neighbourhood
     R.cells_a = cells_from_rows(moved_rows, R.g2);
     if (na == ag) R.cells_n = R.cells_a;

@@ -3,7 +3,7 @@
 # tools/stamp_step, the phase-stamp diagnostic)
 set -o pipefail
 if [ "$1" = build ]; then
-  for v in base STORES UPDOBS DUPSAMPLE; do
+  for v in base STORES ROWS DUPSAMPLE; do
     f=""; [ $v != base ] && f="-DCOG_ABLATE_$v"
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off $f -Iinclude -Igym-eldorado_amd/csrc \
         tools/ablate.cpp -o tools/ablate_$v || exit 1
@@ -12,6 +12,6 @@ if [ "$1" = build ]; then
       -Igym-eldorado_amd/csrc tools/stamp_step.cpp -o tools/stamp_step || exit 1
   exit 0
 fi
-for v in base STORES UPDOBS DUPSAMPLE; do
+for v in base STORES ROWS DUPSAMPLE; do
   printf "%-8s " $v; timeout -k 10 60 tools/ablate_$v 65536 3000 || exit 1
 done
