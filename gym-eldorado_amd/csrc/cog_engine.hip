@@ -1039,6 +1039,15 @@ DEV uint4 pack_player(const PState &P) {
 }
 DEV bool ne4(const uint4 &a, const uint4 &b) { return ((a.x ^ b.x) | (a.y ^ b.y) | (a.z ^ b.z) | (a.w ^ b.w)) != 0u; }
 
+// shop slots with cards left (or, with the market full, the slots in the market): the shop
+// mask's availability half (cards.cpp:109-121); sh4 = ObsData dwords 4..8 (the 18 shop bytes)
+DEV uint32_t shop_avail_of(const uint32_t *sh4, uint32_t n_in_market, uint32_t in_market) {
+  uint32_t nz = 0;
+#pragma unroll
+  for (int q = 0; q < 5; q++) nz |= bools4(sh4[q]) << (4 * q);
+  return n_in_market < COG_MKT_SLOTS ? (nz & 0x3ffffu) : (in_market & 0x3ffffu);
+}
+
 struct RegEnv {
   // EnvPriv granules 0/1 (unpacked fields) and the Info mirror (granule 3, dword 0)
   uint32_t rng, seed, max_steps, turn_counter;
@@ -1052,6 +1061,7 @@ struct RegEnv {
   Heads sel, sta, stn;                                     // selected / stored(ag) / stored(na)
   bool moved;
   uint4 g2;                                                // map bounds + locations
+  uint32_t avail;                                          // shop_avail(), kept across steps
 
   DEV uint32_t n_players() const { return g1x & 0xffu; }
   DEV uint32_t done() const { return g1x >> 24; }
@@ -1255,17 +1265,13 @@ struct RegEnv {
     return m;
   }
   // shop mask bits 1..18 (cards.cpp:109-121) + bit 0
-  DEV uint32_t shop_avail() const {
-    uint32_t nz = 0;
-#pragma unroll
-    for (int q = 0; q < 5; q++) nz |= bools4(sh[4 + q]) << (4 * q);
-    return n_in_market() < COG_MKT_SLOTS ? (nz & 0x3ffffu) : (in_market & 0x3ffffu);
-  }
+  DEV uint32_t shop_avail() const { return shop_avail_of(sh + 4, n_in_market(), in_market); }
+  // shop mask bits from `avail`, the cached shop_avail() (it changes only with a purchase)
   DEV uint32_t shop_bits(float coins) const {
     const uint32_t afford = (coins > 1.f ? kCostMask1 : 0u) | (coins > 2.f ? kCostMask2 : 0u) |
                             (coins > 3.f ? kCostMask3 : 0u) | (coins > 4.f ? kCostMask4 : 0u) |
                             (coins > 5.f ? kCostMask5 : 0u);
-    return 1u | ((shop_avail() & afford) << 1);
+    return 1u | ((avail & afford) << 1);
   }
   // special actions (cards.cpp:8-36, the remove lambda environment.cpp:156-158) on the stored
   // mask `m` of the current agent and the selected mask, for the acting player (:183-186)
@@ -1458,6 +1464,7 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
         nim = (nim - 1u) & 0xffu;
       }
       R.set_n_in_market(nim);
+      R.avail = R.shop_avail();                            // (after the market bookkeeping)
       if (!P.next_card_free) {
         r2 = r2 - (float)cardf(kCost, ty);
         phase = (phase + 1) % 3;
@@ -1538,6 +1545,7 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
 // 16-B granules that differ from it (and nothing else).
 struct Snap {
   uint4 g0, g1, g2;                   // EnvPriv granules 0, 1, 2
+  uint32_t avail;                     // shop_avail_of(sh, g1): refreshed by a purchase
   uint32_t info_steps;                // EnvPriv granule 3, dword 0
   uint4 sh[3];                        // ObsData 16128..16175: phase, resources, shop
   MBits sel;                          // selected mask
@@ -1558,6 +1566,8 @@ DEV void load_env(const DevState &s, size_t i, Snap &S) {          // records at
   S.sh[0] = sh4[0];
   S.sh[1] = sh4[1];
   S.sh[2] = sh4[2];
+  const uint32_t w[5] = {S.sh[1].x, S.sh[1].y, S.sh[1].z, S.sh[1].w, S.sh[2].x};
+  S.avail = shop_avail_of(w, (S.g1.y >> 8) & 0xffu, S.g1.z);
 }
 DEV uint8_t *deck_ptr(const DevState &s, size_t i, int p) {
   return s.obs + i * COG_OBS_BYTES + COG_OBS_PLAYER0 + COG_OBS_PLAYER_STRIDE * p;
@@ -1579,6 +1589,7 @@ DEV void regs_env(RegEnv &R, const Snap &S) {
   R.g1x = S.g1.x; R.g1y = S.g1.y; R.in_market = S.g1.z; R.flags = S.g1.w;
   R.info_steps = S.info_steps;
   R.g2 = S.g2;
+  R.avail = S.avail;
   R.moved = false;
   R.sel = heads_of(S.sel);
 #pragma unroll
@@ -1872,6 +1883,7 @@ __global__ void __launch_bounds__(64) k_env_rollout(DevState s, int steps, uint3
       S.g0 = make_uint4(R.rng, R.seed, R.max_steps, R.turn_counter);
       S.g1 = make_uint4(R.g1x, R.g1y, R.in_market, R.flags);
       S.g2 = R.g2;
+      S.avail = R.avail;
       S.info_steps = R.info_steps;
 #pragma unroll
       for (int k = 0; k < 3; k++) S.sh[k] = make_uint4(R.sh[4 * k], R.sh[4 * k + 1], R.sh[4 * k + 2], R.sh[4 * k + 3]);
