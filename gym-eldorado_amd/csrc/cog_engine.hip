@@ -1154,17 +1154,15 @@ struct RegEnv {
       for (uint32_t i = 0; i < n; i++) {
         const uint32_t k = P.n_in_draw;                    // piles of <= 31: division-free draw
         const uint32_t T = bcast8((k <= 31u ? uid_small(rng, k) : uid_fast(rng, k)) + 1u);
-        uint32_t c = 0;
-#pragma unroll
-        for (int q = 0; q < 6; q++)                        // bytes with prefix <= t: bit 7 clear
-          c += __popc(~((pre[q] | 0x80808080u) - T) & (q < 5 ? 0x80808080u : 0x80u));
-#pragma unroll
-        for (int q = 0; q < 6; q++) {                      // prefix sums of types >= c drop by one
-          const int s8 = min(max(8 * ((int)c - 4 * q), 0), 32);   // (>= 1 there: no borrow)
-          pre[q] -= s8 >= 32 ? 0u : 0x01010101u << s8;
+        uint32_t above = 0;                                // types whose prefix sum is > t: bit 7
+#pragma unroll                                             // of (0x80 + p) - (t + 1), no borrows;
+        for (int q = 0; q < 6; q++) {                      // they are the types >= the drawn card
+          const uint32_t g = ((pre[q] | 0x80808080u) - T) & (q < 5 ? 0x80808080u : 0x80u);
+          above += __popc(g);
+          pre[q] -= g >> 7;                                // (>= 1 there: no borrow)
         }
         P.n_in_draw = (k - 1u) & 0xffu;
-        dm |= 1u << c;
+        dm |= 1u << (COG_N_CARDTYPES - above);
       }
       // the pile back from its prefix sums (nondecreasing bytes < 128: no borrows), and the drawn
       // counts (old pile - new pile, no borrows either) added to the hand: byte k of the draw
