@@ -1130,6 +1130,30 @@ struct RegEnv {
     sel.play = 1u | (h << 1);
     sel.spec = 1u | ((h & kSpecialBits) << 1);
   }
+  // the pile back from its prefix sums (nondecreasing bytes < 128: no borrows), and the drawn
+  // counts (old pile - new pile, no borrows either) added to the hand: byte k of the draw
+  // pile's dword grid is hand byte 21 + k.  The selected mask gains the drawn types (its
+  // play_special bits only ever hold special types, so setting is all the reference's
+  // per-card assignment does).
+  DEV void draw_rebuild(const uint32_t pre[6], uint32_t dm) {
+    uint32_t h[6], prevp = 0;
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+      const uint32_t nd = pre[q] - fsh8(pre[q], prevp, 3);   // p[k] - p[k-1]
+      prevp = pre[q];
+      if (q < 5) {
+        h[q] = d[q] - nd;
+        d[q] = nd;
+      } else {
+        h[5] = (d[5] - nd) & 0xffu;
+        d[5] = (d[5] & 0xffffff00u) | (nd & 0xffu);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 6; q++) d[5 + q] = add8(d[5 + q], fsh8(h[q], q ? h[q - 1] : 0u, 3));
+    sel.play |= dm << 1;
+    sel.spec |= (dm & kSpecialBits) << 1;
+  }
   // Deck::draw (cards.cpp:183-211).  n_in_draw == sum(draw[]) mod 256 (every Deck operation keeps
   // it), so the scan for the t-th card ends inside the pile.  While the pile holds < 128 cards
   // (always in valid play) the scan runs on byte-wise prefix sums, four types per dword: the card
@@ -1149,7 +1173,36 @@ struct RegEnv {
     uint32_t total = d[5] & 0xffu;                         // exact (no u8 wrap) pile total
 #pragma unroll
     for (int q = 0; q < 5; q++) total = sum8(d[q], total);
-    if (total == P.n_in_draw && total < 128u) {            // every prefix sum fits in 7 bits
+    // The draws' generator states are jumped to independently (x 16807^j): with every draw's
+    // value below kSmallSafe (no rejection for any pile of <= 31) they are the states the
+    // sequential draws reach, and the n uniforms need no serial chain.  n <= COG_HAND_SIZE.
+    const uint32_t K0 = P.n_in_draw;
+    uint32_t xs[COG_HAND_SIZE];
+    bool seq = K0 > 31u || n > (uint32_t)COG_HAND_SIZE;
+#pragma unroll
+    for (int j = 0; j < COG_HAND_SIZE; j++) {
+      xs[j] = mr_jump(rng, mr_pow(j + 1));
+      seq |= (uint32_t)j < n && xs[j] - 1u >= kSmallSafe;
+    }
+    if (total == P.n_in_draw && total < 128u && !seq) {
+      uint32_t dm = 0;                                     // types drawn
+#pragma unroll
+      for (int j = 0; j < COG_HAND_SIZE; j++) {
+        const uint32_t live = (uint32_t)j < n ? 0x80808080u : 0u;
+        const uint32_t T = bcast8(uid_small_accepted(xs[j] - 1u, max(K0 - (uint32_t)j, 1u)) + 1u);
+        uint32_t above = 0;                                // as below
+#pragma unroll
+        for (int q = 0; q < 6; q++) {
+          const uint32_t g = ((pre[q] | 0x80808080u) - T) & (q < 5 ? live : (live & 0x80u));
+          above += __popc(g);
+          pre[q] -= g >> 7;
+        }
+        dm |= live ? 1u << (COG_N_CARDTYPES - above) : 0u;
+      }
+      if (n) rng = n == 1u ? xs[0] : n == 2u ? xs[1] : n == 3u ? xs[2] : xs[3];
+      P.n_in_draw = (K0 - n) & 0xffu;
+      draw_rebuild(pre, dm);
+    } else if (total == P.n_in_draw && total < 128u) {     // every prefix sum fits in 7 bits
       uint32_t dm = 0;                                     // types drawn
       for (uint32_t i = 0; i < n; i++) {
         const uint32_t k = P.n_in_draw;                    // piles of <= 31: division-free draw
@@ -1164,28 +1217,7 @@ struct RegEnv {
         P.n_in_draw = (k - 1u) & 0xffu;
         dm |= 1u << (COG_N_CARDTYPES - above);
       }
-      // the pile back from its prefix sums (nondecreasing bytes < 128: no borrows), and the drawn
-      // counts (old pile - new pile, no borrows either) added to the hand: byte k of the draw
-      // pile's dword grid is hand byte 21 + k.  The selected mask gains the drawn types (its
-      // play_special bits only ever hold special types, so setting is all the reference's
-      // per-card assignment does).
-      uint32_t h[6], prevp = 0;
-#pragma unroll
-      for (int q = 0; q < 6; q++) {
-        const uint32_t nd = pre[q] - fsh8(pre[q], prevp, 3);   // p[k] - p[k-1]
-        prevp = pre[q];
-        if (q < 5) {
-          h[q] = d[q] - nd;
-          d[q] = nd;
-        } else {
-          h[5] = (d[5] - nd) & 0xffu;
-          d[5] = (d[5] & 0xffffff00u) | (nd & 0xffu);
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 6; q++) d[5 + q] = add8(d[5 + q], fsh8(h[q], q ? h[q - 1] : 0u, 3));
-      sel.play |= dm << 1;
-      sel.spec |= (dm & kSpecialBits) << 1;
+      draw_rebuild(pre, dm);
     } else {
       for (uint32_t i = 0; i < n; i++) {
         const uint32_t t = uid_fast(rng, P.n_in_draw);
@@ -1375,6 +1407,22 @@ DEV uint2 cells_from_rows(const CellRows &c, const uint4 &g2) {
 
 // cog_env::step (environment.cpp:91-224) for the acting player ag == agent, every action kind.
 // Returns true when the episode ends (finish_episode runs on the stored state afterwards).
+#if defined(COG_ABLATE_DUPENDTURN) || defined(COG_ABLATE_DUPPLAY) || defined(COG_ABLATE_DUPUPDOBS)
+// diagnostic timing builds only: a part of the step run a second time on a laundered copy of the
+// registers (results discarded), to measure its marginal cost without changing the dynamics
+DEV void dup_launder(RegEnv &R2) {
+#pragma unroll
+  for (int k = 0; k < 28; k++) asm volatile("" : "+v"(R2.d[k]));
+  asm volatile("" : "+v"(R2.rng), "+v"(R2.P.n_in_hand), "+v"(R2.P.n_in_draw), "+v"(R2.sel.play), "+v"(R2.sel.spec));
+}
+DEV void dup_sink(const RegEnv &R2) {
+  uint32_t x = R2.rng ^ R2.P.n_in_hand ^ R2.P.n_in_draw ^ R2.sel.play ^ R2.sel.spec ^ R2.P.n_active;
+#pragma unroll
+  for (int k = 0; k < 28; k++) x ^= R2.d[k];
+  asm volatile("" ::"v"(x));
+}
+#endif
+
 DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i, int na PH_PARAM) {
   const int ag = (int)R.agent();
   PState &P = R.P;
@@ -1397,6 +1445,9 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
   }
   if (a_play) {                                            // Player::play_card (player.cpp:45-60)
     const int c = a_play - 1;
+#ifdef COG_ABLATE_DUPPLAY
+    { RegEnv R2 = R; dup_launder(R2); R2.leave_hand(c, false); pile_add<COG_DECK_ACTIVE>(R2.d, c, 1u); dup_sink(R2); }
+#endif
     if (phase == COG_PHASE_MOVEMENT) {
       r0 = (float)cardf(kRes0, c); r1 = (float)cardf(kRes1, c); r2 = (float)cardf(kRes2, c);
     } else if (phase == COG_PHASE_BUYING) {
@@ -1494,6 +1545,10 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
   }
   bool cur_is_ag = true;
   if (P.has_won || phase == COG_PHASE_INACTIVE) {          // maybe_end_turn -> next_agent
+#ifdef COG_ABLATE_DUPENDTURN
+    { RegEnv R2 = R; dup_launder(R2); R2.discard_all(); const int nd2 = COG_HAND_SIZE - (int)R2.P.n_in_hand;
+      if (nd2 > 0) R2.draw((uint32_t)nd2); dup_sink(R2); }
+#endif
     P.n_active = 0;                                        // Player::end_turn (player.cpp:170-180)
     R.discard_all();
     const int n_draw = COG_HAND_SIZE - (int)P.n_in_hand;
@@ -1526,6 +1581,14 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
 #ifndef COG_ABLATE_UPDOBS                                  // diagnostic timing builds only
   if (phase == COG_PHASE_MOVEMENT) mv = R.move_bits(cc, r0, r1, r2, cur_is_ag ? P.n_active : R.na_active);
   else if (phase == COG_PHASE_BUYING) sp = R.shop_bits(r2);
+#endif
+#ifdef COG_ABLATE_DUPUPDOBS
+  { RegEnv R2 = R; float q0 = r0, q1 = r1, q2 = r2; uint2 c2 = cc; uint32_t na2 = cur_is_ag ? P.n_active : R.na_active;
+    asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(c2.x), "+v"(c2.y), "+v"(na2), "+v"(R2.avail));
+    uint32_t m2 = 1u, s2 = 1u;
+    if (phase == COG_PHASE_MOVEMENT) m2 = R2.move_bits(c2, q0, q1, q2, na2);
+    else if (phase == COG_PHASE_BUYING) s2 = R2.shop_bits(q2);
+    asm volatile("" ::"v"(m2 ^ s2 ^ R2.flags)); }
 #endif
   stc.move = mv;
   stc.shop = sp;

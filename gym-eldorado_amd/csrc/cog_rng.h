@@ -88,4 +88,19 @@ COG_HD uint32_t uid_small(uint32_t &x, uint32_t k) {       // k in [1, 31]
 // every draw a k in [1, 31] can reject has r >= range - 30 (range mod k <= 30)
 constexpr uint32_t kSmallSafe = kUrngRange - 31u;
 
+// Jump-ahead: the state j steps on is x * 16807^j mod (2^31 - 1), so the states of several
+// consecutive draws are independent products instead of a serial chain.
+constexpr uint32_t kMinstdM = 0x7fffffffu;
+constexpr uint32_t mr_pow(uint32_t j) {
+  uint64_t v = 1;
+  for (uint32_t i = 0; i < j; i++) v = v * 16807u % kMinstdM;
+  return (uint32_t)v;
+}
+COG_HD uint32_t mr_jump(uint32_t x, uint32_t c) {          // x * c mod (2^31 - 1), x, c < 2^31
+  const uint64_t p = (uint64_t)x * c;                      // < 2^62
+  const uint32_t s = (uint32_t)(p & kMinstdM) + (uint32_t)(p >> 31);   // <= 2^32 - 2
+  const uint32_t r = (s & kMinstdM) + (s >> 31);          // <= 2^31
+  return r >= kMinstdM ? r - kMinstdM : r;
+}
+
 }  // namespace cog

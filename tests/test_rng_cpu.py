@@ -25,6 +25,19 @@ extern "C" void run(const uint32_t *x0, const uint32_t *k, uint32_t n, int which
     xout[i] = x;
   }
 }
+// mr_jump(x, 16807^j) for j = 1..4 against j sequential mr_next steps
+extern "C" uint32_t run_jump(const uint32_t *x0, uint32_t n) {
+  uint32_t bad = 0;
+  const uint32_t c[4] = {cog::mr_pow(1), cog::mr_pow(2), cog::mr_pow(3), cog::mr_pow(4)};
+  for (uint32_t i = 0; i < n; i++) {
+    uint32_t x = x0[i];
+    for (int j = 0; j < 4; j++) {
+      cog::mr_next(x);
+      bad += cog::mr_jump(x0[i], c[j]) != x;
+    }
+  }
+  return bad;
+}
 """
 
 
@@ -36,6 +49,8 @@ def lib(tmp_path_factory):
     subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", f"-I{CSRC}", str(src), "-o", str(so)], check=True)
     lib = ctypes.CDLL(str(so))
     lib.run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    lib.run_jump.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+    lib.run_jump.restype = ctypes.c_uint32
     return lib
 
 
@@ -84,3 +99,12 @@ def test_random_states(lib, which, kmax):
     ref, xref = call(lib, 0, x0, k)
     got, xgot = call(lib, which, x0, k)
     assert np.array_equal(ref, got) and np.array_equal(xref, xgot)
+
+
+def test_jump_ahead(lib):
+    """The draw's jump-ahead states (x * 16807^j mod 2^31-1) equal j sequential steps: random
+    states plus the extremes of the state space."""
+    rng = np.random.default_rng(11)
+    x0 = np.concatenate([np.array([1, 2, 16807, P - 2, P - 1, 2 ** 30, 2 ** 31 - 2], dtype=np.uint64),
+                         rng.integers(1, P, size=1_000_000, dtype=np.uint64)]).astype(np.uint32)
+    assert lib.run_jump(x0.ctypes.data, len(x0)) == 0
