@@ -1162,17 +1162,18 @@ struct RegEnv {
   DEV void draw(uint32_t n) {
     if (P.n_in_draw < n) move_discard_to_draw();
     if (n > P.n_in_draw) n = P.n_in_draw;
+    // pre[q] byte j: draw[0] + .. + draw[4q+j].  The in-dword prefix sums take byte shifts
+    // (alignbyte: kept from being fused into quarter-rate multiplies by 0x01010101); the running
+    // total before dword q (exact, no u8 wrap) is a separate chain of byte-sum adds.
     uint32_t pre[6], carry = 0;
 #pragma unroll
-    for (int q = 0; q < 6; q++) {                          // pre[q] byte j: draw[0] + .. + draw[4q+j]
+    for (int q = 0; q < 6; q++) {
       const uint32_t x = q < 5 ? d[q] : (d[5] & 0xffu);
-      const uint32_t p1 = x + (x << 8);
-      pre[q] = p1 + (p1 << 16) + bcast8(carry);
-      carry = pre[q] >> 24;
+      const uint32_t p1 = x + fsh8(x, 0u, 3);              // x + (x << 8)
+      pre[q] = p1 + fsh8(p1, 0u, 2) + bcast8(carry);       // + (p1 << 16)
+      carry = sum8(x, carry);
     }
-    uint32_t total = d[5] & 0xffu;                         // exact (no u8 wrap) pile total
-#pragma unroll
-    for (int q = 0; q < 5; q++) total = sum8(d[q], total);
+    const uint32_t total = carry;                          // pile total
     // The draws' generator states are jumped to independently (x 16807^j): with every draw's
     // value below kSmallSafe (no rejection for any pile of <= 31) they are the states the
     // sequential draws reach, and the n uniforms need no serial chain.  n <= COG_HAND_SIZE.
