@@ -1134,11 +1134,12 @@ struct RegEnv {
   // counts (old pile - new pile, no borrows either) added to the hand: byte k of the draw
   // pile's dword grid is hand byte 21 + k.  The selected mask gains the drawn types (its
   // play_special bits only ever hold special types, so setting is all the reference's
-  // per-card assignment does).
+  // per-card assignment does).  Only the first NQ dwords of the pile can hold cards.
+  template <int NQ>
   DEV void draw_rebuild(const uint32_t pre[6], uint32_t dm) {
-    uint32_t h[6], prevp = 0;
+    uint32_t h[6] = {0u, 0u, 0u, 0u, 0u, 0u}, prevp = 0;
 #pragma unroll
-    for (int q = 0; q < 6; q++) {
+    for (int q = 0; q < NQ; q++) {
       const uint32_t nd = pre[q] - fsh8(pre[q], prevp, 3);   // p[k] - p[k-1]
       prevp = pre[q];
       if (q < 5) {
@@ -1150,7 +1151,7 @@ struct RegEnv {
       }
     }
 #pragma unroll
-    for (int q = 0; q < 6; q++) d[5 + q] = add8(d[5 + q], fsh8(h[q], q ? h[q - 1] : 0u, 3));
+    for (int q = 0; q < 6 && q <= NQ; q++) d[5 + q] = add8(d[5 + q], fsh8(h[q], q ? h[q - 1] : 0u, 3));
     sel.play |= dm << 1;
     sel.spec |= (dm & kSpecialBits) << 1;
   }
@@ -1159,15 +1160,28 @@ struct RegEnv {
   // (always in valid play) the scan runs on byte-wise prefix sums, four types per dword: the card
   // is the number of types whose prefix sum is <= t.  Otherwise -- stale-mask driving can wrap a
   // count to 255 (Q23) -- card by card, as the reference scans (the guard only raises the flag).
+  //
+  // The prefix-sum work covers the dwords of the pile that can hold cards: the end of a turn asks
+  // the wave (ballot) whether any of its drawing lanes has a card of type >= 8 in its draw pile
+  // after the reshuffle; if none has, only dwords 0-1 are scanned (the types above hold prefix
+  // sums equal to the pile total, never drawn and never changed).  Results are the same either way.
+  template <bool SPAN>
   DEV void draw(uint32_t n) {
     if (P.n_in_draw < n) move_discard_to_draw();
     if (n > P.n_in_draw) n = P.n_in_draw;
+    if (SPAN && !__builtin_amdgcn_ballot_w64((d[2] | d[3] | d[4] | (d[5] & 0xffu)) != 0u)) draw_n<2>(n);
+    else draw_n<6>(n);
+    P.n_in_hand = (P.n_in_hand + n) & 0xffu;
+  }
+  template <int NQ>
+  DEV void draw_n(uint32_t n) {
+    constexpr uint32_t NT = NQ < 6 ? 4 * NQ : COG_N_CARDTYPES;   // types covered
     // pre[q] byte j: draw[0] + .. + draw[4q+j].  The in-dword prefix sums take byte shifts
     // (alignbyte: kept from being fused into quarter-rate multiplies by 0x01010101); the running
     // total before dword q (exact, no u8 wrap) is a separate chain of byte-sum adds.
     uint32_t pre[6], carry = 0;
 #pragma unroll
-    for (int q = 0; q < 6; q++) {
+    for (int q = 0; q < NQ; q++) {
       const uint32_t x = q < 5 ? d[q] : (d[5] & 0xffu);
       const uint32_t p1 = x + fsh8(x, 0u, 3);              // x + (x << 8)
       pre[q] = p1 + fsh8(p1, 0u, 2) + bcast8(carry);       // + (p1 << 16)
@@ -1193,16 +1207,16 @@ struct RegEnv {
         const uint32_t T = bcast8(uid_small_accepted(xs[j] - 1u, max(K0 - (uint32_t)j, 1u)) + 1u);
         uint32_t above = 0;                                // as below
 #pragma unroll
-        for (int q = 0; q < 6; q++) {
+        for (int q = 0; q < NQ; q++) {
           const uint32_t g = ((pre[q] | 0x80808080u) - T) & (q < 5 ? live : (live & 0x80u));
           above += __popc(g);
           pre[q] -= g >> 7;
         }
-        dm |= live ? 1u << (COG_N_CARDTYPES - above) : 0u;
+        dm |= live ? 1u << (NT - above) : 0u;
       }
       if (n) rng = n == 1u ? xs[0] : n == 2u ? xs[1] : n == 3u ? xs[2] : xs[3];
       P.n_in_draw = (K0 - n) & 0xffu;
-      draw_rebuild(pre, dm);
+      draw_rebuild<NQ>(pre, dm);
     } else if (total == P.n_in_draw && total < 128u) {     // every prefix sum fits in 7 bits
       uint32_t dm = 0;                                     // types drawn
       for (uint32_t i = 0; i < n; i++) {
@@ -1210,15 +1224,15 @@ struct RegEnv {
         const uint32_t T = bcast8((k <= 31u ? uid_small(rng, k) : uid_fast(rng, k)) + 1u);
         uint32_t above = 0;                                // types whose prefix sum is > t: bit 7
 #pragma unroll                                             // of (0x80 + p) - (t + 1), no borrows;
-        for (int q = 0; q < 6; q++) {                      // they are the types >= the drawn card
+        for (int q = 0; q < NQ; q++) {                     // they are the types >= the drawn card
           const uint32_t g = ((pre[q] | 0x80808080u) - T) & (q < 5 ? 0x80808080u : 0x80u);
           above += __popc(g);
           pre[q] -= g >> 7;                                // (>= 1 there: no borrow)
         }
         P.n_in_draw = (k - 1u) & 0xffu;
-        dm |= 1u << (COG_N_CARDTYPES - above);
+        dm |= 1u << (NT - above);
       }
-      draw_rebuild(pre, dm);
+      draw_rebuild<NQ>(pre, dm);
     } else {
       for (uint32_t i = 0; i < n; i++) {
         const uint32_t t = uid_fast(rng, P.n_in_draw);
@@ -1234,7 +1248,6 @@ struct RegEnv {
         sel.spec = set_bit(sel.spec, (int)c + 1, is_special((int)c));
       }
     }
-    P.n_in_hand = (P.n_in_hand + n) & 0xffu;
   }
   // card c leaves the hand (Deck::activate / play_immediate / remove_immediate, cards.cpp:242-290)
   DEV void leave_hand(int c, bool rem_rule) {
@@ -1309,11 +1322,11 @@ struct RegEnv {
   DEV void apply_special(int special, Heads &m) {
     switch (special) {
       case COG_SPECIAL_DRAW2:
-      case COG_SPECIAL_DRAW3: draw(special == COG_SPECIAL_DRAW2 ? 2u : 3u); break;
+      case COG_SPECIAL_DRAW3: draw<false>(special == COG_SPECIAL_DRAW2 ? 2u : 3u); break;
       case COG_SPECIAL_DRAW1_REMOVE1:
       case COG_SPECIAL_DRAW2_REMOVE2: {
         const uint32_t k = special == COG_SPECIAL_DRAW1_REMOVE1 ? 1u : 2u;
-        draw(k);
+        draw<false>(k);
         P.n_removes = k;
         m.rem = m.play;                                    // mask.remove = mask.play
         sel.play = 1u;                                     // disable_playing
@@ -1408,7 +1421,8 @@ DEV uint2 cells_from_rows(const CellRows &c, const uint4 &g2) {
 
 // cog_env::step (environment.cpp:91-224) for the acting player ag == agent, every action kind.
 // Returns true when the episode ends (finish_episode runs on the stored state afterwards).
-#if defined(COG_ABLATE_DUPENDTURN) || defined(COG_ABLATE_DUPPLAY) || defined(COG_ABLATE_DUPUPDOBS)
+#if defined(COG_ABLATE_DUPENDTURN) || defined(COG_ABLATE_DUPPLAY) || defined(COG_ABLATE_DUPUPDOBS) || \
+    defined(COG_ABLATE_DUPDISCARD) || defined(COG_ABLATE_DUPDRAW)
 // diagnostic timing builds only: a part of the step run a second time on a laundered copy of the
 // registers (results discarded), to measure its marginal cost without changing the dynamics
 DEV void dup_launder(RegEnv &R2) {
@@ -1546,15 +1560,25 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
   }
   bool cur_is_ag = true;
   if (P.has_won || phase == COG_PHASE_INACTIVE) {          // maybe_end_turn -> next_agent
-#ifdef COG_ABLATE_DUPENDTURN
-    { RegEnv R2 = R; dup_launder(R2); R2.discard_all(); const int nd2 = COG_HAND_SIZE - (int)R2.P.n_in_hand;
-      if (nd2 > 0) R2.draw((uint32_t)nd2); dup_sink(R2); }
+#if defined(COG_ABLATE_DUPENDTURN) || defined(COG_ABLATE_DUPDISCARD) || defined(COG_ABLATE_DUPDRAW)
+    {
+      RegEnv R2 = R;
+      dup_launder(R2);
+#ifndef COG_ABLATE_DUPDRAW
+      R2.discard_all();
+#endif
+      const int nd2 = COG_HAND_SIZE - (int)R2.P.n_in_hand;
+#ifndef COG_ABLATE_DUPDISCARD
+      if (nd2 > 0) R2.draw<true>((uint32_t)nd2);
+#endif
+      dup_sink(R2);
+    }
 #endif
     P.n_active = 0;                                        // Player::end_turn (player.cpp:170-180)
     R.discard_all();
     const int n_draw = COG_HAND_SIZE - (int)P.n_in_hand;
     PH(9);
-    if (n_draw > 0) R.draw((uint32_t)n_draw);
+    if (n_draw > 0) R.draw<true>((uint32_t)n_draw);
     PH(10);
     R.sta = R.sel;                                         // save_actionmask
     R.set_agent((uint32_t)na);
