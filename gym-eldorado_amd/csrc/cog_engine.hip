@@ -1091,32 +1091,39 @@ struct RegEnv {
   }
 
   // Deck::discard_all_active + discard_all_played (cards.cpp:219-232): discard += active + played,
-  // four types per dword (active and played re-aligned to the discard pile's dword grid)
+  // four types per dword (active and played re-aligned to the discard pile's dword grid).
+  // NQ = 2: the deck holds no card of type >= 8 (only dwords 0-1 of each pile's grid can change)
+  template <int NQ>
   DEV void discard_all() {
     uint32_t D[6];
 #pragma unroll
-    for (int q = 0; q < 6; q++)
+    for (int q = 0; q < NQ; q++)
       D[q] = add8(add8(d[21 + q], fsh8(d[11 + q], d[10 + q], 2)), fsh8(d[16 + q], d[15 + q], 3));
 #pragma unroll
-    for (int q = 0; q < 5; q++) d[21 + q] = D[q];
-    d[26] = (d[26] & 0xffffff00u) | (D[5] & 0xffu);        // discard[20]; bytes 105.. are padding
+    for (int q = 0; q < NQ && q < 5; q++) d[21 + q] = D[q];
+    if (NQ == 6) d[26] = (d[26] & 0xffffff00u) | (D[5] & 0xffu);   // discard[20]; bytes 105.. are padding
     d[10] &= 0x0000ffffu;                                  // active[0..1] ..
 #pragma unroll
-    for (int q = 11; q < 21; q++) d[q] = 0u;               // .. played[20]: bytes 42..83 = 0
+    for (int q = 11; q < 21; q++)                          // .. played[20]: bytes 42..83 = 0
+      if (NQ == 6 || q == 11 || q == 12 || q == 15 || q == 16 || q == 17) d[q] = 0u;
   }
   // Deck::move_discard_to_draw (cards.cpp:234-240): both piles start on a dword
+  template <int NQ>
   DEV void move_discard_to_draw() {
     uint32_t n = P.n_in_draw;
 #pragma unroll
-    for (int q = 0; q < 5; q++) {
+    for (int q = 0; q < NQ && q < 5; q++) {
       n = sum8(d[21 + q], n);
       d[q] = add8(d[q], d[21 + q]);
       d[21 + q] = 0u;
     }
-    const uint32_t last = d[26] & 0xffu;                   // discard[20] -> draw[20]
-    d[5] = (d[5] & 0xffffff00u) | ((d[5] + last) & 0xffu);
-    d[26] &= 0xffffff00u;
-    P.n_in_draw = (n + last) & 0xffu;
+    if (NQ == 6) {
+      const uint32_t last = d[26] & 0xffu;                 // discard[20] -> draw[20]
+      d[5] = (d[5] & 0xffffff00u) | ((d[5] + last) & 0xffu);
+      d[26] &= 0xffffff00u;
+      n += last;
+    }
+    P.n_in_draw = n & 0xffu;
   }
   DEV uint32_t hand_bits() const {                         // hand[k] > 0 for k < 21
     uint32_t h = 0;
@@ -1161,16 +1168,15 @@ struct RegEnv {
   // is the number of types whose prefix sum is <= t.  Otherwise -- stale-mask driving can wrap a
   // count to 255 (Q23) -- card by card, as the reference scans (the guard only raises the flag).
   //
-  // The prefix-sum work covers the dwords of the pile that can hold cards: the end of a turn asks
-  // the wave (ballot) whether any of its drawing lanes has a card of type >= 8 in its draw pile
-  // after the reshuffle; if none has, only dwords 0-1 are scanned (the types above hold prefix
-  // sums equal to the pile total, never drawn and never changed).  Results are the same either way.
-  template <bool SPAN>
+  // NQ = 2: the deck holds no card of type >= 8 (the wave's `wide` ballot at the end of the turn,
+  // from the per-player flag a purchase of such a card sets): only dwords 0-1 of the pile grid
+  // are scanned -- the types above hold prefix sums equal to the pile total, never drawn and never
+  // changed.  Results are the same either way.
+  template <int NQ>
   DEV void draw(uint32_t n) {
-    if (P.n_in_draw < n) move_discard_to_draw();
+    if (P.n_in_draw < n) move_discard_to_draw<NQ>();
     if (n > P.n_in_draw) n = P.n_in_draw;
-    if (SPAN && !__builtin_amdgcn_ballot_w64((d[2] | d[3] | d[4] | (d[5] & 0xffu)) != 0u)) draw_n<2>(n);
-    else draw_n<6>(n);
+    draw_n<NQ>(n);
     P.n_in_hand = (P.n_in_hand + n) & 0xffu;
   }
   template <int NQ>
@@ -1234,6 +1240,7 @@ struct RegEnv {
       }
       draw_rebuild<NQ>(pre, dm);
     } else {
+      P.pad = 1u;                                          // the deck's "wide" flag (see draw)
       for (uint32_t i = 0; i < n; i++) {
         const uint32_t t = uid_fast(rng, P.n_in_draw);
         uint32_t c = pile_scan<COG_DECK_DRAW>(d, t);
@@ -1267,6 +1274,7 @@ struct RegEnv {
   // reference's scan (cards.cpp:196-201) may run past the pile on an inconsistent deck
   DEV void take_from_active(uint32_t n, bool discard) {
     const uint32_t avail = P.n_active;
+    P.pad = 1u;                                            // the deck's "wide" flag (see draw)
     if (n > avail) {
       if (discard) flags |= F_Q24_CLAMP;
       n = avail;
@@ -1322,11 +1330,11 @@ struct RegEnv {
   DEV void apply_special(int special, Heads &m) {
     switch (special) {
       case COG_SPECIAL_DRAW2:
-      case COG_SPECIAL_DRAW3: draw<false>(special == COG_SPECIAL_DRAW2 ? 2u : 3u); break;
+      case COG_SPECIAL_DRAW3: draw<6>(special == COG_SPECIAL_DRAW2 ? 2u : 3u); break;
       case COG_SPECIAL_DRAW1_REMOVE1:
       case COG_SPECIAL_DRAW2_REMOVE2: {
         const uint32_t k = special == COG_SPECIAL_DRAW1_REMOVE1 ? 1u : 2u;
-        draw<false>(k);
+        draw<6>(k);
         P.n_removes = k;
         m.rem = m.play;                                    // mask.remove = mask.play
         sel.play = 1u;                                     // disable_playing
@@ -1449,6 +1457,10 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
   P.steps_taken = (P.steps_taken + 1) & 0xffu;
   float r0 = __uint_as_float(R.sh[1]), r1 = __uint_as_float(R.sh[2]), r2 = __uint_as_float(R.sh[3]);
   const int a_play = act[0], a_special = act[1], a_remove = act[2], a_move = act[3], a_shop = act[4];
+  // the deck's "wide" flag (sticky): set by any action naming a card type >= 8 (a valid one names a
+  // card the deck holds; an invalid one -- stale masks, host actions -- may create the type by u8
+  // wrap-around), by a purchase of such a type, and by the scans that can run past a pile
+  if (max(max(a_play, a_special), a_remove) > 8) P.pad = 1u;
   int special = COG_SPECIAL_NONE;
   CellRows moved_rows = {};
   if (a_move && !a_play && !a_special) {                   // the destination's neighbourhood: its
@@ -1534,6 +1546,7 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
         phase = (phase + 1) % 3;
       }
       pile_add<COG_DECK_DISCARD>(R.d, ty, 1u);
+      if (ty >= 8) P.pad = 1u;                             // the deck's "wide" flag (see draw)
       P.n_added_cards = (P.n_added_cards + 1) & 0xffu;
     } else if (a_remove) {
       const int c = a_remove - 1;
@@ -1565,20 +1578,25 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
       RegEnv R2 = R;
       dup_launder(R2);
 #ifndef COG_ABLATE_DUPDRAW
-      R2.discard_all();
+      R2.discard_all<6>();
 #endif
       const int nd2 = COG_HAND_SIZE - (int)R2.P.n_in_hand;
 #ifndef COG_ABLATE_DUPDISCARD
-      if (nd2 > 0) R2.draw<true>((uint32_t)nd2);
+      if (nd2 > 0) R2.draw<6>((uint32_t)nd2);
 #endif
       dup_sink(R2);
     }
 #endif
     P.n_active = 0;                                        // Player::end_turn (player.cpp:170-180)
-    R.discard_all();
     const int n_draw = COG_HAND_SIZE - (int)P.n_in_hand;
     PH(9);
-    if (n_draw > 0) R.draw<true>((uint32_t)n_draw);
+    if (__builtin_amdgcn_ballot_w64(P.pad != 0u)) {        // a deck of the wave holds a type >= 8
+      R.discard_all<6>();
+      if (n_draw > 0) R.draw<6>((uint32_t)n_draw);
+    } else {
+      R.discard_all<2>();
+      if (n_draw > 0) R.draw<2>((uint32_t)n_draw);
+    }
     PH(10);
     R.sta = R.sel;                                         // save_actionmask
     R.set_agent((uint32_t)na);
