@@ -1577,13 +1577,22 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
     {
       RegEnv R2 = R;
       dup_launder(R2);
-#ifndef COG_ABLATE_DUPDRAW
-      R2.discard_all<6>();
-#endif
       const int nd2 = COG_HAND_SIZE - (int)R2.P.n_in_hand;
-#ifndef COG_ABLATE_DUPDISCARD
-      if (nd2 > 0) R2.draw<6>((uint32_t)nd2);
+      if (__builtin_amdgcn_ballot_w64(R2.P.pad != 0u)) {
+#ifndef COG_ABLATE_DUPDRAW
+        R2.discard_all<6>();
 #endif
+#ifndef COG_ABLATE_DUPDISCARD
+        if (nd2 > 0) R2.draw<6>((uint32_t)nd2);
+#endif
+      } else {
+#ifndef COG_ABLATE_DUPDRAW
+        R2.discard_all<2>();
+#endif
+#ifndef COG_ABLATE_DUPDISCARD
+        if (nd2 > 0) R2.draw<2>((uint32_t)nd2);
+#endif
+      }
       dup_sink(R2);
     }
 #endif

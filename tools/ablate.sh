@@ -3,7 +3,7 @@
 # tools/stamp_step, the phase-stamp diagnostic)
 set -o pipefail
 if [ "$1" = build ] || [ "$1" = build-base ]; then
-  vs="base DUPSAMPLE DUPENDTURN DUPDISCARD DUPDRAW DUPPLAY DUPUPDOBS"; [ "$1" = build-base ] && vs=base
+  vs="${ABL:-base DUPSAMPLE DUPENDTURN DUPDISCARD DUPDRAW DUPPLAY DUPUPDOBS}"; [ "$1" = build-base ] && vs=base
   for v in $vs; do
     f=""; [ $v != base ] && f="-DCOG_ABLATE_$v"
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -mllvm -amdgpu-sched-strategy=max-ilp $f -Iinclude -Igym-eldorado_amd/csrc \
@@ -16,6 +16,6 @@ if [ "$1" = build ] || [ "$1" = build-base ]; then
       -Igym-eldorado_amd/csrc tools/stamp_step.cpp -o tools/stamp_step || exit 1
   exit 0
 fi
-for v in base DUPSAMPLE DUPENDTURN DUPDISCARD DUPDRAW DUPPLAY DUPUPDOBS; do
+for v in ${ABL:-base DUPSAMPLE DUPENDTURN DUPDISCARD DUPDRAW DUPPLAY DUPUPDOBS}; do
   printf "%-8s " $v; timeout -k 10 60 tools/ablate_$v 65536 3000 || exit 1
 done
