@@ -1462,16 +1462,13 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
   // wrap-around), by a purchase of such a type, and by the scans that can run past a pile
   if (max(max(a_play, a_special), a_remove) > 8) P.pad = 1u;
   int special = COG_SPECIAL_NONE;
-  CellRows moved_rows = {};
-  if (a_move && !a_play && !a_special) {                   // the destination's neighbourhood: its
-    const int lx = (int8_t)((R.g2.z >> (8 * ag)) & 0xffu) + dir_dx(a_move);   // loads are issued
-    const int ly = (int8_t)((R.g2.w >> (8 * ag)) & 0xffu) + dir_dy(a_move);   // first, used last
-    R.g2.z = (R.g2.z & ~(0xffu << (8 * ag))) | (((uint32_t)lx & 0xffu) << (8 * ag));
-    R.g2.w = (R.g2.w & ~(0xffu << (8 * ag))) | (((uint32_t)ly & 0xffu) << (8 * ag));
-    moved_rows = cell_rows(s.cgrid + i * COG_CELLS, R.g2, lx, ly);
-  }
-  if (a_play) {                                            // Player::play_card (player.cpp:45-60)
-    const int c = a_play - 1;
+  // A wave whose lanes only play cards or pass, with no free move / free card / pending removes
+  // / move in progress (all of the canonical selected-mask loop), takes the short
+  // path: one uniform branch instead of one divergent skip per action kind.
+  const bool rare = (a_special | a_remove | a_move | a_shop) != 0 ||
+                    (P.next_move_free | P.next_card_free | P.n_removes | P.mip) != 0u;
+  const bool wave_simple = !__builtin_amdgcn_ballot_w64(rare);
+  auto play_card = [&](int c) {                            // Player::play_card (player.cpp:45-60)
 #ifdef COG_ABLATE_DUPPLAY
     { RegEnv R2 = R; dup_launder(R2); R2.leave_hand(c, false); pile_add<COG_DECK_ACTIVE>(R2.d, c, 1u); dup_sink(R2); }
 #endif
@@ -1485,89 +1482,105 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
     pile_add<COG_DECK_ACTIVE>(R.d, c, 1u);
     P.n_active = (P.n_active + 1) & 0xffu;
     P.idx_last = (uint32_t)c;
-  } else if (a_special) {                                  // play_special (environment.cpp:108-114)
-    const int c = a_special - 1;
-    const bool single = cardf(kSingle, c) != 0u;
-    R.leave_hand(c, single);                               // remove_immediate / play_immediate
-    if (!single) pile_add<COG_DECK_PLAYED>(R.d, c, 1u);
-    special = (int)cardf(kSpecial, c);
-  } else if (a_move) {                                     // move (environment.cpp:115-127)
-    const uint32_t c = R.use_cell_dyn(R.cells_a, a_move);
-    if (!P.next_move_free) {                               // Player::handle_requirement (:141-162)
-      const uint32_t req = COG_HEX_REQ(c), n = COG_HEX_N(c);
-      if (req < 3) {
-        const float left = (req == 0 ? r0 : req == 1 ? r1 : r2) - (float)n;
-        r0 = req == 0 ? left : 0.f;
-        r1 = req == 1 ? left : 0.f;
-        r2 = req == 2 ? left : 0.f;
-        if (!P.mip) {                                      // Deck::play_last_activated
-          const int l = (int)P.idx_last;
-          P.n_active = (P.n_active - 1) & 0xffu;
-          dk_addv<COG_DECK_ACTIVE, 105>(R.d, COG_DECK_ACTIVE + l, 0xffu);
-          if (!cardf(kSingle, l)) dk_addv<COG_DECK_PLAYED, 105>(R.d, COG_DECK_PLAYED + l, 1u);
-          P.mip = 1;
+  };
+  CellRows moved_rows = {};
+  if (wave_simple) {
+    if (a_play) play_card(a_play - 1);
+    else phase = (phase + 1) % 3;                          // pass: next phase
+  } else {
+    if (a_move && !a_play && !a_special) {                   // the destination's neighbourhood: its
+      const int lx = (int8_t)((R.g2.z >> (8 * ag)) & 0xffu) + dir_dx(a_move);   // loads are issued
+      const int ly = (int8_t)((R.g2.w >> (8 * ag)) & 0xffu) + dir_dy(a_move);   // first, used last
+      R.g2.z = (R.g2.z & ~(0xffu << (8 * ag))) | (((uint32_t)lx & 0xffu) << (8 * ag));
+      R.g2.w = (R.g2.w & ~(0xffu << (8 * ag))) | (((uint32_t)ly & 0xffu) << (8 * ag));
+      moved_rows = cell_rows(s.cgrid + i * COG_CELLS, R.g2, lx, ly);
+    }
+    if (a_play) {
+      play_card(a_play - 1);
+    } else if (a_special) {                                  // play_special (environment.cpp:108-114)
+      const int c = a_special - 1;
+      const bool single = cardf(kSingle, c) != 0u;
+      R.leave_hand(c, single);                               // remove_immediate / play_immediate
+      if (!single) pile_add<COG_DECK_PLAYED>(R.d, c, 1u);
+      special = (int)cardf(kSpecial, c);
+    } else if (a_move) {                                     // move (environment.cpp:115-127)
+      const uint32_t c = R.use_cell_dyn(R.cells_a, a_move);
+      if (!P.next_move_free) {                               // Player::handle_requirement (:141-162)
+        const uint32_t req = COG_HEX_REQ(c), n = COG_HEX_N(c);
+        if (req < 3) {
+          const float left = (req == 0 ? r0 : req == 1 ? r1 : r2) - (float)n;
+          r0 = req == 0 ? left : 0.f;
+          r1 = req == 1 ? left : 0.f;
+          r2 = req == 2 ? left : 0.f;
+          if (!P.mip) {                                      // Deck::play_last_activated
+            const int l = (int)P.idx_last;
+            P.n_active = (P.n_active - 1) & 0xffu;
+            dk_addv<COG_DECK_ACTIVE, 105>(R.d, COG_DECK_ACTIVE + l, 0xffu);
+            if (!cardf(kSingle, l)) dk_addv<COG_DECK_PLAYED, 105>(R.d, COG_DECK_PLAYED + l, 1u);
+            P.mip = 1;
+          }
+        } else if (req == COG_REQ_REMOVE || req == COG_REQ_DISCARD) {
+          R.take_from_active(n, req == COG_REQ_DISCARD);
+          r0 = r1 = r2 = 0.f;
+          P.mip = 0;
         }
-      } else if (req == COG_REQ_REMOVE || req == COG_REQ_DISCARD) {
-        R.take_from_active(n, req == COG_REQ_DISCARD);
-        r0 = r1 = r2 = 0.f;
-        P.mip = 0;
+      } else {
+        P.next_move_free = 0;
+        R.enable_playing();
       }
+      P.n_movements++;
+      P.has_won = COG_HEX_END(c);
+      R.moved = true;
     } else {
       P.next_move_free = 0;
-      R.enable_playing();
-    }
-    P.n_movements++;
-    P.has_won = COG_HEX_END(c);
-    R.moved = true;
-  } else {
-    P.next_move_free = 0;
-    if (a_shop) {                                          // Shop::get_card (cards.cpp:123-142)
-      const int k = a_shop - 1;
-      const int ty = shop_type(k);
-      const uint32_t bit = 1u << k;
-      uint32_t nim = R.n_in_market();
-      if (!P.next_card_free) {
-        nim = (nim + ((R.in_market & bit) ? 0u : 1u)) & 0xffu;
-        R.in_market |= bit;
-      }
-      const uint32_t left = (R.shop_byte(k) - 1u) & 0xffu;
-      const int q = 4 + (k >> 2), sh8 = 8 * (k & 3);
-#pragma unroll
-      for (int w = 4; w < 9; w++)
-        if (w == q) R.sh[w] = (R.sh[w] & ~(0xffu << sh8)) | (left << sh8);
-      if (!left && (R.in_market & bit)) {
-        R.in_market &= ~bit;
-        nim = (nim - 1u) & 0xffu;
-      }
-      R.set_n_in_market(nim);
-      R.avail = R.shop_avail();                            // (after the market bookkeeping)
-      if (!P.next_card_free) {
-        r2 = r2 - (float)cardf(kCost, ty);
+      if (a_shop) {                                          // Shop::get_card (cards.cpp:123-142)
+        const int k = a_shop - 1;
+        const int ty = shop_type(k);
+        const uint32_t bit = 1u << k;
+        uint32_t nim = R.n_in_market();
+        if (!P.next_card_free) {
+          nim = (nim + ((R.in_market & bit) ? 0u : 1u)) & 0xffu;
+          R.in_market |= bit;
+        }
+        const uint32_t left = (R.shop_byte(k) - 1u) & 0xffu;
+        const int q = 4 + (k >> 2), sh8 = 8 * (k & 3);
+  #pragma unroll
+        for (int w = 4; w < 9; w++)
+          if (w == q) R.sh[w] = (R.sh[w] & ~(0xffu << sh8)) | (left << sh8);
+        if (!left && (R.in_market & bit)) {
+          R.in_market &= ~bit;
+          nim = (nim - 1u) & 0xffu;
+        }
+        R.set_n_in_market(nim);
+        R.avail = R.shop_avail();                            // (after the market bookkeeping)
+        if (!P.next_card_free) {
+          r2 = r2 - (float)cardf(kCost, ty);
+          phase = (phase + 1) % 3;
+        }
+        pile_add<COG_DECK_DISCARD>(R.d, ty, 1u);
+        if (ty >= 8) P.pad = 1u;                             // the deck's "wide" flag (see draw)
+        P.n_added_cards = (P.n_added_cards + 1) & 0xffu;
+      } else if (a_remove) {
+        const int c = a_remove - 1;
+        R.leave_hand(c, true);                               // Deck::remove_immediate
+        P.n_removes = (P.n_removes - 1) & 0xffu;
+        if (!P.n_removes) R.enable_playing();
+        else special = COG_SPECIAL_SHOP_OFF;
+      } else {                                               // pass: next phase
         phase = (phase + 1) % 3;
+        if (P.n_removes > 0) {
+          P.n_removes = 0;
+          R.enable_playing();
+        }
       }
-      pile_add<COG_DECK_DISCARD>(R.d, ty, 1u);
-      if (ty >= 8) P.pad = 1u;                             // the deck's "wide" flag (see draw)
-      P.n_added_cards = (P.n_added_cards + 1) & 0xffu;
-    } else if (a_remove) {
-      const int c = a_remove - 1;
-      R.leave_hand(c, true);                               // Deck::remove_immediate
-      P.n_removes = (P.n_removes - 1) & 0xffu;
-      if (!P.n_removes) R.enable_playing();
-      else special = COG_SPECIAL_SHOP_OFF;
-    } else {                                               // pass: next phase
-      phase = (phase + 1) % 3;
-      if (P.n_removes > 0) {
-        P.n_removes = 0;
+      if (P.next_card_free) {
+        P.next_card_free = 0;
         R.enable_playing();
       }
     }
-    if (P.next_card_free) {
-      P.next_card_free = 0;
-      R.enable_playing();
-    }
   }
   PH(8);
-  if (P.mip && !a_move) {                                  // the move HEAD, whatever was taken
+  if (!wave_simple && P.mip && !a_move) {                  // the move HEAD, whatever was taken
     P.mip = 0;
     r0 = r1 = r2 = 0.f;
   }
@@ -1620,9 +1633,9 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
   R.sh[0] = (R.sh[0] & ~0xffu) | phase;
   R.sh[1] = __float_as_uint(r0); R.sh[2] = __float_as_uint(r1); R.sh[3] = __float_as_uint(r2);
 #ifndef COG_ABLATE_ROWS                                    // diagnostic timing builds only
-  rows_ready(moved_rows);
+  if (!wave_simple) rows_ready(moved_rows);               // (uniform: converged)
 #endif
-  if (R.moved) {                                           // the mover's new neighbourhood
+  if (!wave_simple && R.moved) {                           // the mover's new neighbourhood
     R.cells_a = cells_from_rows(moved_rows, R.g2);
     if (na == ag) R.cells_n = R.cells_a;
   }
@@ -1645,7 +1658,7 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
   stc.move = mv;
   stc.shop = sp;
   PH(12);
-  if (special != COG_SPECIAL_NONE) {
+  if (!wave_simple && special != COG_SPECIAL_NONE) {
     R.apply_special(special, stc);
     return false;
   }
