@@ -908,10 +908,14 @@ DEV void sample_heads(const Heads &h, uint32_t &rng, uint8_t out[5]) {
   }
   rng = x;
 #pragma unroll
-  for (int j = 0; j < 5; j++) {
-    uint32_t v = k[j] ? (uint32_t)(__ffs(m[j]) - 1) : 0u;
-    if (k[j] >= 2u) v = nth_set_bit(m[j], uid_small_accepted(r[j], k[j]));
-    out[j] = (uint8_t)v;
+  for (int j = 0; j < 5; j++) out[j] = (uint8_t)(k[j] ? (uint32_t)(__ffs(m[j]) - 1) : 0u);
+  if (k[0] >= 2u) out[0] = (uint8_t)nth_set_bit(m[0], uid_small_accepted(r[0], k[0]));
+  // heads 1-4 rarely hold two candidates (the selected mask's special / remove / move / shop
+  // heads): one uniform branch skips them all when no lane of the wave needs arithmetic there
+  if (__builtin_amdgcn_ballot_w64(max(max(k[1], k[2]), max(k[3], k[4])) >= 2u)) {
+#pragma unroll
+    for (int j = 1; j < 5; j++)
+      if (k[j] >= 2u) out[j] = (uint8_t)nth_set_bit(m[j], uid_small_accepted(r[j], k[j]));
   }
 }
 DEV void sample_mask(const uint8_t *mask, uint32_t &rng, uint8_t out[5]) {
@@ -1180,6 +1184,27 @@ struct RegEnv {
     P.n_in_hand = (P.n_in_hand + n) & 0xffu;
   }
   template <int NQ>
+  DEV void draw_fast(uint32_t pre[6], uint32_t n, uint32_t K0, const uint32_t xs[COG_HAND_SIZE]) {
+    constexpr uint32_t NT = NQ < 6 ? 4 * NQ : COG_N_CARDTYPES;   // types covered
+    uint32_t dm = 0;                                     // types drawn
+#pragma unroll
+    for (int j = 0; j < COG_HAND_SIZE; j++) {
+      const uint32_t live = (uint32_t)j < n ? 0x80808080u : 0u;
+      const uint32_t T = bcast8(uid_small_accepted(xs[j] - 1u, max(K0 - (uint32_t)j, 1u)) + 1u);
+      uint32_t above = 0;                                // as below
+#pragma unroll
+      for (int q = 0; q < NQ; q++) {
+        const uint32_t g = ((pre[q] | 0x80808080u) - T) & (q < 5 ? live : (live & 0x80u));
+        above += __popc(g);
+        pre[q] -= g >> 7;
+      }
+      dm |= live ? 1u << (NT - above) : 0u;
+    }
+    if (n) rng = n == 1u ? xs[0] : n == 2u ? xs[1] : n == 3u ? xs[2] : xs[3];
+    P.n_in_draw = (K0 - n) & 0xffu;
+    draw_rebuild<NQ>(pre, dm);
+  }
+  template <int NQ>
   DEV void draw_n(uint32_t n) {
     constexpr uint32_t NT = NQ < 6 ? 4 * NQ : COG_N_CARDTYPES;   // types covered
     // pre[q] byte j: draw[0] + .. + draw[4q+j].  The in-dword prefix sums take byte shifts
@@ -1205,24 +1230,9 @@ struct RegEnv {
       xs[j] = mr_jump(rng, mr_pow(j + 1));
       seq |= (uint32_t)j < n && xs[j] - 1u >= kSmallSafe;
     }
-    if (total == P.n_in_draw && total < 128u && !seq) {
-      uint32_t dm = 0;                                     // types drawn
-#pragma unroll
-      for (int j = 0; j < COG_HAND_SIZE; j++) {
-        const uint32_t live = (uint32_t)j < n ? 0x80808080u : 0u;
-        const uint32_t T = bcast8(uid_small_accepted(xs[j] - 1u, max(K0 - (uint32_t)j, 1u)) + 1u);
-        uint32_t above = 0;                                // as below
-#pragma unroll
-        for (int q = 0; q < NQ; q++) {
-          const uint32_t g = ((pre[q] | 0x80808080u) - T) & (q < 5 ? live : (live & 0x80u));
-          above += __popc(g);
-          pre[q] -= g >> 7;
-        }
-        dm |= live ? 1u << (NT - above) : 0u;
-      }
-      if (n) rng = n == 1u ? xs[0] : n == 2u ? xs[1] : n == 3u ? xs[2] : xs[3];
-      P.n_in_draw = (K0 - n) & 0xffu;
-      draw_rebuild<NQ>(pre, dm);
+    const bool fast = total == P.n_in_draw && total < 128u && !seq;
+    if (fast) {
+      draw_fast<NQ>(pre, n, K0, xs);
     } else if (total == P.n_in_draw && total < 128u) {     // every prefix sum fits in 7 bits
       uint32_t dm = 0;                                     // types drawn
       for (uint32_t i = 0; i < n; i++) {
