@@ -89,3 +89,31 @@ def test_sampler_draws_at_the_rejection_boundary(cg):
                 s.sample(masks)
                 o.sample(masks)
                 assert po.named_equal(s.get_actions(), o.actions) is None, (j, r)
+
+
+@pytest.mark.parametrize("seed", [5, 77])
+def test_arbitrary_in_range_actions_against_oracle(cg, seed):
+    """Host actions drawn at random within each head's range, masks ignored: cards played that
+    are not in hand (u8 wrap-around), any card type including >= 8 (the deck's wide flag and the
+    narrow/wide pile scans), moves into any neighbour, purchases whatever the coins.  The
+    reference defines these byte by byte (only indices past a head are out of bounds), so the
+    engine must match the oracle on every named field and on the hazard flags."""
+    n, steps = 256, 400
+    rng = np.random.default_rng(seed)
+    env = cg.vec.get_vec_env(n)()
+    orc = po.OracleVec(n)
+    env.reset(seed, 4, 3, cg.HARD, 60, False)
+    orc.reset(seed, 4, 3, 2, 60)
+    top = (21, 21, 21, 6, 18)
+    for t in range(steps):
+        a = np.zeros(n, dtype=po.ACTION)
+        head = rng.integers(0, 6, size=n)                # one head per env (5: pass), sometimes two
+        for k, nm in enumerate(po.ACTION.names):
+            v = rng.integers(1, top[k] + 1, size=n).astype(np.uint8)
+            pick = (head == k) | (rng.random(n) < 0.05)
+            a[nm] = np.where(pick, v, 0)
+        env.step(a)
+        orc.step(a)
+        assert_same(env, orc, f"seed {seed} step {t}")
+    haz, per = env.hazards()
+    assert np.array_equal(per, orc.flags()), "hazard flags differ"
