@@ -73,11 +73,24 @@ COG_HD uint32_t small_past(uint32_t k) {                  // k * (range / k), k 
   const uint32_t j = k < 13 ? k - 1u : (k < 25 ? k - 13u : k - 25u);
   return kUrngRange - ((uint32_t)(tab >> (5u * j)) & 31u);
 }
-COG_HD uint32_t uid_small_accepted(uint32_t r, uint32_t k) {   // r < small_past(k): the value
-  const uint32_t past = small_past(k);
+COG_HD uint32_t small_mod(uint32_t k) {                    // range mod k, k in [1, 31]
+  const uint64_t tab = k < 13 ? kRes5_1 : (k < 25 ? kRes5_13 : kRes5_25);
+  const uint32_t j = k < 13 ? k - 1u : (k < 25 ? k - 13u : k - 25u);
+  return (uint32_t)(tab >> (5u * j)) & 31u;
+}
+// r < small_past(k): the value, in 32-bit arithmetic after the one 64-bit product r k < 2^36.
+// With r k = y 2^31 + l (l < 2^31) and range = 2^31 - 3: q0 = floor(r k / range) is y + c, where
+// c = 1 exactly when l + 3 y + 3 >= 2^31, and the remainder is l + 3 y - 3 c (mod 2^31).  Then
+// (q0 + 1)(range - m) <= r k  <=>  rem + (q0 + 1) m >= range  (m = range mod k <= 30).
+COG_HD uint32_t uid_small_accepted(uint32_t r, uint32_t k) {
   const uint64_t rk = (uint64_t)r * k;
-  const uint32_t q = div_range(rk);
-  return q + ((uint64_t)(q + 1u) * past <= rk ? 1u : 0u);
+  const uint32_t lo = (uint32_t)rk, l = lo & 0x7fffffffu;
+  const uint32_t y = (uint32_t)(rk >> 31);                 // <= 31
+  const uint32_t S = l + 3u * y + 3u;                      // < 2^31 + 96
+  const uint32_t c = S >> 31;
+  const uint32_t q0 = y + c;
+  const uint32_t rem = S - (c ? 0x80000000u : 3u);
+  return q0 + (rem + (q0 + 1u) * small_mod(k) >= kUrngRange ? 1u : 0u);
 }
 COG_HD uint32_t uid_small(uint32_t &x, uint32_t k) {       // k in [1, 31]
   const uint32_t past = small_past(k);

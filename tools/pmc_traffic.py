@@ -22,7 +22,7 @@ KERNELS = {"void cog::k_env_rollout<0, false>": "k_env_rollout", "void cog::k_en
 
 def engine_hash():
     h = hashlib.sha256()
-    for f in ("cog_engine.hip", "cog_engine.h", "cog_tables.h"):
+    for f in ("cog_engine.hip", "cog_engine.h", "cog_tables.h", "cog_rng.h"):
         with open(os.path.join(ROOT, "gym-eldorado_amd", "csrc", f), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]
