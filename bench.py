@@ -5,30 +5,37 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (BASELINE.json metric "env-steps/sec at n_envs=65536, 4 players"; config C5): each
-rank owns 65,536 independent environments (4 players, HARD, n_pieces=3, max_steps=100000,
-env seeds 12345 + global index, sampler seeds the same) resident in its GPU's HBM.  One step =
-the reference loop `sample(selected_action_masks); step(actions)` (benchmarks/benchmarks.py:
-47-51) for every env, run by the runner's on-device loop: a persistent kernel performs C steps
-per launch (default 1000), keeping each env's state on-chip between steps and storing every
-step's outputs (ObsData / ActionMask / Info records, rewards, dones, agent_selection, sampled
-actions, sampler state) in place in HBM -- the same bytes a one-launch-per-step run leaves
-(tests/test_gpu_rollout.py).  No host round-trip.  Environments shard by index across ranks
-with no collective on the data path (weak scaling); the only collectives are the timing
-barrier and the max/sum of scalars.
+Headline workload (BASELINE.json metric "env-steps/sec at n_envs=65536, 4 players"; configs
+C4/C5): 65,536 environments IN TOTAL, split by index across the N ranks (8,192 per GPU at N=8:
+strong scaling), 4 players, HARD, n_pieces=3, max_steps=100000, env seeds 12345 + global index,
+sampler seeds the same, everything resident in HBM.  One step = the reference loop
+`sample(selected_action_masks); step(actions)` (benchmarks/benchmarks.py:47-51) for every env,
+run by the runner's on-device loop: one persistent kernel performs min(C, K) steps per launch,
+keeping each env's state on-chip between steps and storing every step's outputs (ObsData /
+ActionMask / Info records, rewards, dones, agent_selection, sampled actions) in place in HBM --
+the bytes a one-launch-per-step run leaves (tests/test_gpu_rollout.py).  No host round-trip
+(C5).  No collective on the data path; the only collectives are the timing barrier and the
+max/sum of scalars (gloo).
 
-Also reported:
-  roofline      the dominant kernel (k_env_rollout): algorithmic bytes per launch from SURVEY
-                8d's per-env-step table, split into its reads (419 B: needed once per launch,
-                the state then stays on-chip) and its writes (381 B: every step) ->
-                n x (419 + C x 381) B per launch / average launch time (HIP events on the
-                runner's stream); traffic = PMC HBM bytes per launch (rocprofv3 --pmc, gfx950
-                corrections) measured on this exact engine source, else null.
-  per_launch    the same workload with one kernel launch per step (k_env_step<selected>):
-                throughput, kernel time and its roofline at the full 800 B/env-step.
-  encode        the map-observation encode kernel (k_encode, reset path): 18,432 B/env.
-  cpu_baseline  the C oracle (port of the reference) on the host cores in the reference
-                ThreadedRunner shape, bounded sample (rank 0, N=1 only).
+Also reported (rank 0; the extra lines only at N=1, so a scaling run stays short):
+  roofline       the dominant kernel k_env_rollout.  It is instruction-issue bound, not HBM
+                 bound: bound "valu-issue"; achieved = VALU wave-instructions per second (the
+                 per-wave-step VALU count of a rocprofv3 --pmc pass of this exact engine source,
+                 profiles/pmc_profile.json, x waves x steps / the launch time measured here with
+                 HIP events); peak = 1,024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU
+                 (MI355X_MICROARCH.md).  `hbm` holds the counter-measured HBM traffic (FETCH x 2
+                 + WRITE, gfx950 corrections) and SURVEY 8d's 800 B/env-step figure beside it.
+  shard_sizes    rollout us/step at the N=1 batch (65,536 on one GPU) and the N=8 shard (8,192)
+  per_launch     one kernel launch per step (k_env_step<selected>)
+  host_loop      the reference's numpy loop through the host API at C2 (256, EASY) and the C4
+                 shard (8,192, HARD, runner.sample(); runner.step_sync()), D2H bytes per step
+  full_dynamics  stored-mask driver (moves, shop, specials), max_steps 30: auto-resets with
+                 device map generation inside the rollout
+  reset, sample  time_reset / time_sample equivalents (benchmarks/benchmarks.py:53-69)
+  encode         the map-observation encode kernel (reset path), 18,432 B/env, beside a measured
+                 device copy peak
+  cpu_baseline   the C oracle (port of the reference) on the host cores in the reference
+                 ThreadedRunner shape, bounded sample (rank 0, N=1 only)
 """
 from __future__ import annotations
 
@@ -41,31 +48,31 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gym-eldorado_amd"))
 
-N_ENVS_PER_GPU = 65536
+N_ENVS_TOTAL = 65536
+N_SHARD8 = N_ENVS_TOTAL // 8
 SEED = 12345
 N_PLAYERS, N_PIECES, MAX_STEPS = 4, 3, 100000
-STEP_BYTES = 800            # algorithmic bytes per env-step ...
-STEP_READ_BYTES = 419       # ... of which reads: mask 92, sampler rng 4, action 5, selected mask 92,
-                            # deck 105, phase/res/shop 31, 6 neighbour features 42, scalars 48
-STEP_WRITE_BYTES = 381      # ... and writes: action 5, rng 4, selected mask 92, deck 105, stored
-                            # mask 92, phase/res/shop 31, scalars 48, done/agent/info 4
-ENCODE_BYTES = 18432        # algorithmic bytes per encoded env (16,128 written + 2,304 read)
+STEP_BYTES = 800            # algorithmic bytes per env-step of sample + step
+WRITEBACK_BYTES = 1234      # D2H / write-back bytes per env-step (C4)
+ENCODE_BYTES = 18432        # per encoded env (16,128 written + 2,304 read)
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
+N_SIMD, CLOCK_HZ, VALU_CYC = 1024, 2.4e9, 2.0   # 256 CUs x 4 SIMD-32; wave64 VALU = 2 cycles
 METRIC = "env-steps/sec at n_envs=65536, 4 players; bit-exact vs C++ ref"
+HAZ_ERASE_PAST = 0x02       # map.cpp:727 erase past the end: GCC>=13 libstdc++ semantics (oracle-pinned)
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10000)
+    ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--envs", type=int, default=N_ENVS_PER_GPU, help="envs per GPU")
+    ap.add_argument("--envs-total", type=int, default=N_ENVS_TOTAL, help="envs over all ranks")
     ap.add_argument("--chunk", type=int, default=1000, help="rollout steps per kernel launch")
-    ap.add_argument("--no-per-launch", action="store_true", help="skip the one-launch-per-step line")
+    ap.add_argument("--no-extras", action="store_true", help="headline + roofline only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline wall time")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline wall time")
     ap.add_argument("--profile-steps", type=int, default=0,
-                    help="only run warmup + this many steps (for rocprofv3 captures); no JSON checks")
+                    help="only run warmup + this many rollout steps (rocprofv3 captures); no JSON checks")
     return ap.parse_args()
 
 
@@ -80,23 +87,21 @@ class Dist:
             import torch
             import torch.distributed as dist
             self.torch = torch
-            if torch.cuda.is_available():
-                torch.cuda.set_device(self.local)
             dist.init_process_group("gloo")      # timing barrier / max only: no data-path collective
             self.dist = dist
             self.pg = True
         else:
             try:
                 import torch
-                if torch.cuda.is_available():
-                    self.torch = torch
+                self.torch = torch
             except Exception:
                 self.torch = None
 
     def barrier_sync(self, runner):
         runner.sync()
-        if self.torch is not None and self.torch.cuda.is_available():
-            self.torch.cuda.synchronize()
+        t = self.torch
+        if t is not None and t.cuda.is_available():
+            t.cuda.synchronize()
         if self.pg:
             self.dist.barrier()
 
@@ -119,23 +124,104 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def load_pmc_traffic(kernel, steps_per_launch):
-    """Per-launch HBM bytes for `kernel` measured by rocprofv3 --pmc (profiles/pmc_traffic.json,
-    written by tools/pmc_traffic.py); None unless measured on this exact engine source with the
-    same envs and steps per launch."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def device_of(d):
+    """This rank's GPU: LOCAL_RANK, unless COG_DEVICE pins it (several ranks on one GPU)."""
+    v = os.environ.get("COG_DEVICE")
+    return int(v) if v else d.local
+
+
+def load_profile():
+    """profiles/pmc_profile.json (tools/pmc_profile.py) when it was measured on this exact engine
+    source; else None."""
     try:
         sys.path.insert(0, os.path.join(ROOT, "tools"))
-        from pmc_traffic import engine_hash
-        with open(p) as f:
-            d = json.load(f)
-        e = d.get(kernel)
-        if (e and e.get("envs_per_launch") == N_ENVS_PER_GPU and e.get("steps_per_launch", 1) == steps_per_launch
-                and d.get("engine_sha") == engine_hash()):
-            return float(e["bytes_per_launch"])
+        from pmc_profile import engine_hash
+        with open(os.path.join(ROOT, "profiles", "pmc_profile.json")) as f:
+            p = json.load(f)
+        return p if p.get("engine_sha") == engine_hash() else None
     except Exception:
-        pass
-    return None
+        return None
+
+
+def make(cg, n, base, device, difficulty=None, max_steps=MAX_STEPS, device_views=True, stored=False):
+    env = cg.vec.get_vec_env(n)(device=device)
+    smp = cg.vec.get_vec_sampler(n)(base, device=device)
+    env.reset(base, N_PLAYERS, N_PIECES, cg.HARD if difficulty is None else difficulty, max_steps, False)
+    runner = cg.vec.get_runner(n)(env, smp, None, device_views=device_views, stored_masks=stored)
+    return env, smp, runner
+
+
+def kernel_time(runner, steps_per_launch, launches):
+    """Seconds per launch: HIP events on the runner's stream around `launches` back-to-back
+    launches of `steps_per_launch` steps (the per-launch average rocprofv3's kernel trace gives)."""
+    runner.set_chunk(steps_per_launch)
+    runner.set_timing(True)
+    runner.rollout(steps_per_launch * launches)
+    ms, steps_done = runner.kernel_time()
+    runner.set_timing(False)
+    return ms / 1e3 / max(steps_done, 1) * steps_per_launch
+
+
+def us_per_step(cg, n, device, steps=1000):
+    env, smp, runner = make(cg, n, SEED, device)
+    runner.set_chunk(steps)
+    runner.rollout(200)
+    runner.sync()
+    t = kernel_time(runner, steps, 2)
+    del runner, smp, env
+    return t / steps * 1e6
+
+
+def host_loop(cg, n, difficulty, device, steps, use_runner):
+    """The reference's loop through the host API with numpy views every step."""
+    env = cg.vec.get_vec_env(n)(device=device)
+    smp = cg.vec.get_vec_sampler(n)(SEED, device=device)
+    env.reset(SEED, N_PLAYERS, N_PIECES, difficulty, MAX_STEPS, False)
+    masks, acts = env.selected_action_masks, smp.get_actions()
+    runner = cg.vec.get_runner(n)(env, smp, None) if use_runner else None
+
+    def one():
+        if runner is not None:
+            runner.sample()
+            runner.step_sync()
+        else:
+            smp.sample(masks)
+            env.step(acts)
+    for _ in range(20):
+        one()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    wall = time.perf_counter() - t0
+    # bytes over PCIe per env-step: D2H ObsData tail (1,088) + selected mask, info, rewards, done,
+    # agent (338) + actions (64); H2D actions (64) [+ masks H2D 128 + actions D2H 64 without runner]
+    d2h = 1088 + 128 + 192 + 16 + 2 + (64 if use_runner else 64)
+    h2d = 0 if use_runner else 64 + 128
+    return {"value": n * steps / wall, "unit": "env-steps/s", "ms_per_step": wall / steps * 1e3,
+            "envs": n, "steps": steps, "d2h_bytes_per_env_step": d2h, "h2d_bytes_per_env_step": h2d,
+            "survey_8d_writeback_bytes": WRITEBACK_BYTES,
+            "pcie_GBs": n * (d2h + h2d) * steps / wall / 1e9,
+            "loop": "runner.sample(); runner.step_sync()" if use_runner else "sampler.sample(masks); env.step(actions)"}
+
+
+def copy_peak_gbs(d):
+    """A device-to-device copy of 2 GiB (torch), read + write bytes per second."""
+    t = d.torch
+    if t is None or not t.cuda.is_available():
+        return None
+    dev = t.device("cuda", device_of(d))
+    a = t.empty(1 << 31, dtype=t.uint8, device=dev)
+    b = t.empty_like(a)
+    b.copy_(a)
+    e0, e1 = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        b.copy_(a)
+    e1.record()
+    e1.synchronize()
+    s = e0.elapsed_time(e1) / 1e3 / 5
+    del a, b
+    return 2.0 * (1 << 31) / s / 1e9
 
 
 def cpu_baseline(seconds):
@@ -154,49 +240,87 @@ def cpu_baseline(seconds):
     smp = po.OracleSampler(n, SEED)
     vec.reset(SEED, N_PLAYERS, N_PIECES, 2, MAX_STEPS)
     best = None
-    for threads in sorted({1, max(1, cores // 2), cores}):
+    counts = sorted({1, max(1, cores // 2), cores})
+    for threads in counts:
         po.run_threaded(vec, smp, 50, threads)                     # warm-up
         probe = 400
         t = po.run_threaded(vec, smp, probe, threads)
-        steps = max(probe, int(probe * (seconds / 3.0) / max(t, 1e-6)))
+        steps = max(probe, int(probe * (seconds / len(counts)) / max(t, 1e-6)))
         t = po.run_threaded(vec, smp, steps, threads)
         rate = n * steps / t
         if best is None or rate > best[0]:
             best = (rate, threads, steps)
     rate, threads, steps = best
     return {"value": rate, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{n} envs (first {n} of the workload: 4p HARD seed {SEED}) x {steps} steps of "
+            "sample": f"{n} envs (the first {n} of the workload: 4p HARD seed {SEED}) x {steps} steps of "
                       f"sample(selected masks)+step, C oracle, {threads} pinned worker threads "
-                      f"(best of thread counts {sorted({1, max(1, cores // 2), cores})})"}
+                      f"(best of thread counts {counts})"}
+
+
+def roofline(prof, n, k_chunk, launch_s):
+    waves = (n + 63) // 64
+    peak = N_SIMD * CLOCK_HZ / VALU_CYC                   # wave64 VALU instructions per second
+    out = {"bound": "valu-issue", "kernel": "k_env_rollout<selected>", "unit": "VALU wave-instr/s",
+           "peak": peak, "achieved": None, "frac": None, "traffic": None, "kernel_ms": launch_s * 1e3,
+           "steps_per_launch": k_chunk, "envs_per_launch": n}
+    alg = STEP_BYTES * n * k_chunk
+    out["hbm"] = {"survey_8d_bytes_per_launch": alg, "survey_8d_GBs": alg / launch_s / 1e9,
+                  "note": "800 B/env-step (SURVEY 8d) assumes every step reads its state from HBM; "
+                          "the rollout keeps it on-chip, so this rate can exceed the HBM peak"}
+    r = (prof or {}).get("k_env_rollout")
+    if r:
+        per_ws = r["valu_per_wave_step"]
+        achieved = per_ws * waves * k_chunk / launch_s
+        out.update(achieved=achieved, frac=achieved / peak, valu_per_wave_step=per_ws,
+                   salu_per_wave_step=r.get("salu_per_wave_step"),
+                   issue_quads_per_wave_step=r.get("active_inst_any_per_wave_step"),
+                   wait_quads_per_wave_step=r.get("wait_any_per_wave_step"),
+                   wave_quads_per_wave_step=r.get("wave_cycles_per_wave_step"),
+                   lone_wave_frac=achieved / (peak / 2),
+                   note="one 64-env wave per SIMD: a lone wave issues at most one VALU per 4 cycles "
+                        "(lone_wave_frac is against that cap); profiled at %d envs x %d steps per launch"
+                        % (r.get("envs_per_launch", 0), r.get("steps_per_launch", 0)))
+        tr = r.get("bytes_per_step_launch", {})
+        key = str(k_chunk)
+        if key in tr:
+            out["traffic"] = tr[key]
+            out["hbm"]["counter_GBs"] = tr[key] / launch_s / 1e9
+            out["hbm"]["counter_frac"] = tr[key] / launch_s / 1e9 / HBM_PEAK_GBS
+        elif "per_env_step" in r:
+            out["hbm"]["counter_bytes_per_env_step"] = r["per_env_step"]
+    else:
+        out["note"] = "no PMC profile of this engine source (tools/pmc_profile.py): achieved unknown"
+    return out
 
 
 def main():
     args = parse()
     d = Dist(args.gpus)
     import city_of_gold as cg
+    from city_of_gold.shard import shard, shard_seed
 
-    n = args.envs
-    base = SEED + d.rank * n                              # env i of rank r = global index r*n + i
-    env = cg.vec.get_vec_env(n)(device=d.local)
-    smp = cg.vec.get_vec_sampler(n)(base, device=d.local)
+    dev = device_of(d)
+    lo, hi = shard(args.envs_total, d.rank, d.world)       # env i of rank r = global index lo + i
+    n = hi - lo
+    base = shard_seed(SEED, lo)
     t0 = time.time()
-    env.reset(base, N_PLAYERS, N_PIECES, cg.HARD, MAX_STEPS, False)
-    reset_s = time.time() - t0
-    runner = cg.vec.get_runner(n)(env, smp, None, device_views=True)
-    chunk = max(1, args.chunk)
+    env, smp, runner = make(cg, n, base, dev)
+    setup_s = time.time() - t0
+    chunk = max(1, min(args.chunk, max(args.steps, 1)))
     runner.set_chunk(chunk)
 
     runner.rollout(args.warmup)
     d.barrier_sync(runner)
 
-    if args.profile_steps:                                # rocprofv3 captures: both kernels
-        runner.rollout(args.profile_steps)
+    if args.profile_steps:                                # rocprofv3 captures: the rollout at
+        runner.set_chunk(min(args.chunk, args.profile_steps))   # K steps per launch, then 200
+        runner.rollout(args.profile_steps)                 # one-launch-per-step k_env_step's
         d.barrier_sync(runner)
         runner.set_chunk(1)
-        runner.rollout(min(args.profile_steps, 500))
+        runner.rollout(200)
         d.barrier_sync(runner)
         if d.rank == 0:
-            print(json.dumps({"profile_steps": args.profile_steps, "envs": n, "chunk": chunk}))
+            print(json.dumps({"profile_steps": args.profile_steps, "envs": n, "chunk": args.chunk}))
         d.close()
         return
 
@@ -210,45 +334,88 @@ def main():
     total_env_steps = d.sum(float(n) * args.steps)
     value = total_env_steps / wall_max
 
-    # ---- kernel timing for the roofline: HIP events on the runner's stream bracketing one
-    # batch of back-to-back launches (the per-launch average rocprofv3's kernel trace reports)
-    def kernel_time(steps_per_launch, launches):
-        runner.set_chunk(steps_per_launch)
-        runner.set_timing(True)
-        runner.rollout(steps_per_launch * launches)
-        ms, steps_done = runner.kernel_time()
-        runner.set_timing(False)
-        return ms / 1e3 / max(steps_done, 1) * steps_per_launch       # seconds per launch
-
+    # ---- roofline of the dominant kernel at the timed launch length -----------------------
     k_chunk = min(chunk, args.steps)
-    launch_s = kernel_time(k_chunk, max(1, min(args.steps, 2 * k_chunk) // k_chunk))
-    alg_bytes = n * (STEP_READ_BYTES + k_chunk * STEP_WRITE_BYTES)
-    achieved = alg_bytes / launch_s / 1e9
-    traffic = load_pmc_traffic("k_env_rollout", k_chunk)
+    launch_s = kernel_time(runner, k_chunk, max(3, min(20, 4000 // max(k_chunk, 1))))
+    prof = load_profile()
+    roof = roofline(prof, n, k_chunk, launch_s)
 
-    per_launch = None
-    if not args.no_per_launch:
-        pl_steps = min(args.steps, 2000)
-        d.barrier_sync(runner)
+    haz, per = env.hazards()
+    n_erase = int(((per & HAZ_ERASE_PAST) != 0).sum())
+    n_any = int((per != 0).sum())
+    n_erase, n_any = int(d.sum(n_erase)), int(d.sum(n_any))
+
+    extras = {}
+    if d.world == 1 and not args.no_extras:
+        runner.set_chunk(chunk)
+        extras["shard_sizes"] = {"us_per_step_at_%d" % n: launch_s / k_chunk * 1e6 if k_chunk >= 1000 else
+                                 us_per_step(cg, n, dev),
+                                 "us_per_step_at_%d" % N_SHARD8: us_per_step(cg, N_SHARD8, dev),
+                                 "note": "rollout device time per step, 1,000-step launches; the N=8 shard "
+                                         "(8,192 envs = 128 waves) runs one wave per CU on half the CUs"}
+        # one kernel launch per step (the runner's step() path)
+        pl_steps = 500
         runner.set_chunk(1)
+        d.barrier_sync(runner)
         t1 = time.perf_counter()
         runner.rollout(pl_steps)
         d.barrier_sync(runner)
-        pl_wall = d.max(time.perf_counter() - t1)
-        pl_kern = kernel_time(1, pl_steps)
-        pl_ach = STEP_BYTES * n / pl_kern / 1e9
-        per_launch = {"kernel": "k_env_step<selected>", "value": d.sum(float(n) * pl_steps) / pl_wall,
-                      "ms_per_step": pl_wall / pl_steps * 1e3, "kernel_ms": pl_kern * 1e3,
-                      "roofline": {"bound": "hbm", "achieved": pl_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                   "frac": pl_ach / HBM_PEAK_GBS, "traffic": load_pmc_traffic("k_env_step", 1),
-                                   "algorithmic_bytes_per_launch": STEP_BYTES * n}}
-    runner.set_chunk(chunk)
-
-    enc_ms = env.time_encode(20)
-    enc_gbs = ENCODE_BYTES * n / (enc_ms / 1e3) / 1e9
-
-    # parity guard on the benchmarked state: no hazard / error in any env
-    haz, _ = env.hazards()
+        pl_wall = time.perf_counter() - t1
+        pl_kern = kernel_time(runner, 1, pl_steps)
+        tr = ((prof or {}).get("k_env_step") or {}).get("bytes_per_launch")
+        extras["per_launch"] = {"kernel": "k_env_step<selected>", "value": n * pl_steps / pl_wall,
+                                "ms_per_step": pl_wall / pl_steps * 1e3, "kernel_us": pl_kern * 1e6,
+                                "hbm": {"survey_8d_GBs": STEP_BYTES * n / pl_kern / 1e9,
+                                        "survey_8d_frac": STEP_BYTES * n / pl_kern / 1e9 / HBM_PEAK_GBS,
+                                        "traffic": tr,
+                                        "counter_frac": (tr / pl_kern / 1e9 / HBM_PEAK_GBS) if tr else None}}
+        runner.set_chunk(chunk)
+        enc_ms = env.time_encode(20)
+        enc_gbs = ENCODE_BYTES * n / (enc_ms / 1e3) / 1e9
+        cp = copy_peak_gbs(d)
+        extras["encode"] = {"kernel": "k_encode", "ms": enc_ms, "achieved": enc_gbs, "unit": "GB/s",
+                            "frac": enc_gbs / HBM_PEAK_GBS, "copy_peak_GBs": cp,
+                            "frac_of_copy_peak": enc_gbs / cp if cp else None,
+                            "algorithmic_bytes_per_launch": ENCODE_BYTES * n}
+        del runner, smp, env
+        # full dynamics: stored masks (moves, shop, specials), episodes of 30 turns -> auto-resets
+        env, smp, runner = make(cg, n, base, dev, max_steps=30, stored=True)
+        runner.set_chunk(500)
+        runner.rollout(200)
+        d.barrier_sync(runner)
+        fd_steps = 1000
+        t1 = time.perf_counter()
+        runner.rollout(fd_steps)
+        d.barrier_sync(runner)
+        fd_wall = time.perf_counter() - t1
+        env.sync_host()
+        resets = int(env.infos["total_length"].astype(bool).sum())
+        extras["full_dynamics"] = {"value": n * fd_steps / fd_wall, "unit": "env-steps/s",
+                                   "ms_per_step": fd_wall / fd_steps * 1e3, "steps": fd_steps,
+                                   "workload": f"{n} envs, 4p HARD, max_steps 30, stored-mask sampler, "
+                                               "500-step launches, auto-reset with device map generation",
+                                   "envs_with_a_finished_episode": resets}
+        # time_reset / time_sample (benchmarks/benchmarks.py:53-69)
+        t1 = time.perf_counter()
+        reps = 5
+        for r in range(reps):
+            env.reset(SEED + r, N_PLAYERS, N_PIECES, cg.HARD, MAX_STEPS, False)
+        rs = (time.perf_counter() - t1) / reps
+        masks = env.selected_action_masks
+        smp.sample(masks)
+        t1 = time.perf_counter()
+        for _ in range(20):
+            smp.sample(masks)
+        ss = (time.perf_counter() - t1) / 20
+        extras["reset"] = {"envs": n, "s_per_reset_call": rs, "resets_per_s": n / rs,
+                           "note": "env.reset(seed, 4, 3, HARD, ...): device map generation + encode + "
+                                   "host views refresh (1.1 GB D2H of ObsData)"}
+        extras["sample"] = {"envs": n, "ms_per_call": ss * 1e3, "samples_per_s": n / ss,
+                            "note": "sampler.sample(host masks): H2D masks, sampler kernel, D2H actions"}
+        del runner, smp, env
+        extras["host_loop"] = {
+            "C2": host_loop(cg, 256, cg.EASY, dev, 300, False),
+            "C4_shard": host_loop(cg, N_SHARD8, cg.HARD, dev, 100, True)}
 
     if d.rank == 0:
         cpu = None
@@ -263,45 +430,29 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": wall_max / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (procedurally generated maps from seeds; uniform masked random actions)",
             "steps_per_launch": chunk,
             "config": {
-                "workload": "C5: 65536 envs/GPU, 4 players, HARD, n_pieces=3, max_steps=100000, "
-                            "on-device masked sampler over selected_action_masks + step, persistent "
-                            "rollout kernel, every step's AoS outputs stored in HBM",
+                "workload": "C5: 65,536 envs in total over the ranks, 4 players, HARD, n_pieces=3, "
+                            "max_steps=100000, on-device masked sampler over selected_action_masks + step, "
+                            "persistent rollout kernel, every step's AoS outputs stored in HBM",
+                "n_envs_total": args.envs_total,
                 "n_envs_per_gpu": n,
-                "n_envs_total": n * d.world,
                 "seed": SEED,
-                "parallelism": f"env-sharded x{d.world}, no collectives",
+                "parallelism": f"env-sharded x{d.world} by index (runner.h:33-38 block split), no collectives",
             },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "k_env_rollout<selected, lean> + fix-up",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "kernel_ms": launch_s * 1e3,
-                "steps_per_launch": k_chunk,
-                "algorithmic_bytes_per_launch": alg_bytes,
-            },
-            "per_launch": per_launch,
-            "encode": {
-                "kernel": "k_encode",
-                "ms": enc_ms,
-                "achieved": enc_gbs,
-                "unit": "GB/s",
-                "frac": enc_gbs / HBM_PEAK_GBS,
-                "algorithmic_bytes_per_launch": ENCODE_BYTES * n,
-            },
-            "reset_s": reset_s,
-            "hazards_or": int(haz),
+            "roofline": roof,
+            "parity": {"hazard_envs": n_any, "erase_past_envs": n_erase,
+                       "note": "erase_past envs follow map.cpp:727's past-the-end erase with GCC>=13 "
+                               "libstdc++ semantics: pinned by the C oracle, not by a reference run "
+                               "(DESIGN.md 3); every other env's state is pinned by reference digests"},
+            "setup_s": setup_s,
             "cpu_baseline": cpu,
         }
+        out.update(extras)
         print(json.dumps(out), flush=True)
     d.close()
 

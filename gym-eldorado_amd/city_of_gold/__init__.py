@@ -41,7 +41,9 @@ from . import _city_of_gold as _C
 
 Difficulty = _C.Difficulty
 EASY, MEDIUM, HARD = _C.EASY, _C.MEDIUM, _C.HARD
-ObsData, ActionMask, ActionData, Info, DeckObs = _C.ObsData, _C.ActionMask, _C.ActionData, _C.Info, _C.DeckObs
+# record classes (single_env.cpp:34-85); each also acts as its numpy dtype (np.zeros(n, dtype=cg.ActionData))
+from .records import (ActionData, ActionMask, DeckObs, Info, ObsData, PlayerData, PlayerObservation,  # noqa: E402
+                      SharedObservation, action_sampler)
 device_count = _C.device_count
 
 VEC_ENV_CLS = "vec_cog_env_"
@@ -68,9 +70,15 @@ def _make_env_cls(n):
     def __init__(self, device=None):
         _C.VecEnvBase.__init__(self, n, device)
 
+    def step_device(self, d_actions, stream=None):
+        """step() with ActionData records in device memory (a torch tensor's data_ptr()),
+        ordered after torch's current stream unless `stream` (a handle, 0: none) is given."""
+        _C.VecEnvBase.step_device(self, d_actions, stream_handle() if stream is None else int(stream))
+
     doc = (f"Vectorized city of gold environment for {n} environments.\n\n"
            "reset() must be called first to initialize the environments before stepping.")
     return type(VEC_ENV_CLS + str(n), (_C.VecEnvBase,), {"__init__": __init__, "__doc__": doc,
+                                                         "step_device": step_device,
                                                          "__module__": "city_of_gold.vec.sampler"})
 
 
@@ -108,17 +116,32 @@ def _getter(module, prefix, factory):
 DEVICE_VIEWS = ("observations", "selected_action_masks", "rewards", "dones", "agent_selection", "infos")
 
 
-def device_tensors(env, sampler=None):
-    """The env's device views (and the sampler's device actions) as torch tensors, zero copy via
-    DLPack: rows are records, as uint8 bytes (rewards: float32 (N, 4)); they alias the engine
-    state, which the engine updates on its own HIP stream (`env.stream()`), so synchronise
-    (runner.sync() / env.sync_host()) before reading.  The reference's docs suggest TensorDict
-    over copies of the numpy views (docs/source/index.rst:20-26); these need no copy."""
+def device_tensors(env, sampler=None, shard=0):
+    """Shard `shard`'s device views (and the sampler's device actions) as torch tensors, zero
+    copy via DLPack: rows are records, as uint8 bytes (rewards: float32 (N, 4)).  They alias the
+    engine state, which the engine updates on its own HIP stream (env.stream(shard)): before
+    reading them on a torch stream, order that stream after the engine with
+    env.signal_stream(stream_handle(), shard) (or runner.sync()); before the engine consumes
+    tensors torch wrote, env.wait_stream(stream_handle(), shard) (step_device(ptr) does that
+    itself with torch's current stream).  The reference's docs suggest TensorDict over copies of
+    the numpy views (docs/source/index.rst:20-26); these need no copy."""
     import torch
-    out = {nm: torch.from_dlpack(env.dlpack(nm)) for nm in DEVICE_VIEWS}
+    out = {nm: torch.from_dlpack(env.dlpack(nm, shard)) for nm in DEVICE_VIEWS}
     if sampler is not None:
-        out["actions"] = torch.from_dlpack(sampler.dlpack())
+        out["actions"] = torch.from_dlpack(sampler.dlpack()) if sampler.num_shards == 1 else None
     return out
+
+
+def stream_handle(device=None):
+    """torch's current HIP stream on `device` as an int handle (0 without torch), the stream
+    argument of step_device / wait_stream / signal_stream."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            return int(torch.cuda.current_stream(device).cuda_stream)
+    except Exception:
+        pass
+    return 0
 
 
 from .single import cog_env  # noqa: E402  (src/pybind/single_env.cpp: the single-env API)
@@ -134,4 +157,5 @@ for _n in list(range(0, 9)) + [16, 32, 64, 128, 256]:
 del _n, _m
 
 __all__ = ["vec", "Difficulty", "EASY", "MEDIUM", "HARD", "ObsData", "ActionMask", "ActionData", "Info",
-           "DeckObs", "get_vec_env", "get_vec_sampler", "get_runner", "device_count", "device_tensors", "cog_env"]
+           "DeckObs", "SharedObservation", "PlayerData", "PlayerObservation", "action_sampler", "get_vec_env",
+           "get_vec_sampler", "get_runner", "device_count", "device_tensors", "stream_handle", "cog_env"]

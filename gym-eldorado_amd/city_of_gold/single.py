@@ -20,6 +20,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import _city_of_gold as _C
+from .records import Info, _Record
 
 DEFAULTS = dict(n_players=4, n_pieces=3, difficulty=_C.Difficulty.EASY, max_steps=100000, render=False)
 
@@ -40,6 +41,8 @@ class cog_env:
     # ---- environment.h:50-56 -----------------------------------------------------------------
     def init(self, observations, info, rewards, selected_action_masks):
         def rec(a, dtype, what):
+            if isinstance(a, _Record):
+                a = a.record
             a = np.asarray(a)
             if a.dtype != dtype or a.size != 1:
                 raise ValueError(f"{what}: expected one {dtype} record")
@@ -70,6 +73,8 @@ class cog_env:
 
     def step(self, action):
         a = np.zeros(1, dtype=_C.ActionData)
+        if isinstance(action, _Record):
+            action = action.record
         if isinstance(action, np.ndarray) or isinstance(action, np.void):
             src = np.asarray(action).reshape(-1)
             if src.dtype != _C.ActionData or src.size != 1:
@@ -116,7 +121,7 @@ class cog_env:
         return self._done
 
     def get_info(self):
-        return self._v.infos[0]
+        return Info(self._v.infos[0:1].copy())
 
     def get_map(self):
         return self._v.observations[0]["shared"]["map"]

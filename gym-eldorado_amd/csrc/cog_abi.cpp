@@ -1,7 +1,17 @@
 // cog_abi.cpp -- host side of libcog_hip.so: implements the C ABI of include/cog.h on top of the
-// kernels in cog_engine.hip.  Owns device buffers, the per-handle HIP stream, the lazily
-// allocated pinned host views and the asynchronous runner.  No CPU fallback exists: without a
-// gfx950 device every constructor fails with COG_ERR_NODEVICE.
+// kernels in cog_engine.hip.  No CPU fallback exists: without a gfx950 device every constructor
+// fails with COG_ERR_NODEVICE.
+//
+// A handle owns one or more shards: contiguous env ranges, each resident on one GPU with its own
+// HIP stream and device state (the reference ThreadedRunner's contiguous per-worker blocks,
+// runner.h:33-38, with GPUs in place of pinned threads).  Seeds are seed + global index, so the
+// results do not depend on the shard layout.  Host views are pinned; shard k copies into its
+// slice.  Every operation is issued on all shards' streams first and waited for afterwards, so
+// the GPUs of a handle run concurrently.
+//
+// Device layout per shard (one allocation `outs`, so a host-visible step needs two D2H copies:
+// this block and the strided ObsData tail):
+//   [status 64 B][selected masks n x 128][infos n x 192][rewards n x 16][dones n][agents n]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -63,20 +73,54 @@ int dmalloc(T **p, size_t bytes) {
   return COG_OK;
 }
 template <class T>
-int hmalloc(T **p, size_t bytes) {
-  if (hipHostMalloc(reinterpret_cast<void **>(p), bytes ? bytes : 64, hipHostMallocDefault) != hipSuccess)
+int hmalloc(T **p, size_t bytes, unsigned flags = hipHostMallocDefault) {
+  if (hipHostMalloc(reinterpret_cast<void **>(p), bytes ? bytes : 64, flags) != hipSuccess)
     return fail(COG_ERR_OOM, "hipHostMalloc of " + std::to_string(bytes) + " bytes failed");
   return COG_OK;
 }
 
+// the reference runner's block split (runner.h:33-38): n / k per block, the last takes the rest
+std::vector<size_t> block_split(size_t n, int k) {
+  std::vector<size_t> first(k + 1);
+  const size_t b = n / (size_t)k;
+  for (int j = 0; j < k; j++) first[j] = b * (size_t)j;
+  first[k] = n;
+  return first;
+}
+
+constexpr size_t kStatusBytes = 64;
+struct OutLayout {                    // offsets inside a shard's `outs` block (device and host)
+  size_t sel, info, rew, done, agent, total;
+  explicit OutLayout(size_t n) {
+    sel = kStatusBytes;
+    info = sel + n * COG_MASK_BYTES;
+    rew = info + n * COG_INFO_BYTES;
+    done = rew + n * 4 * sizeof(float);
+    agent = done + n;
+    total = agent + n;
+  }
+};
+
 }  // namespace
 
-struct cog_env {
+struct EnvShard {
   int device = 0;
+  size_t first = 0, n = 0;
   hipStream_t stream = nullptr;
+  hipEvent_t ev = nullptr;            // cross-stream ordering (cog_env_wait_stream / signal_stream)
   cog::DevState s{};
+  uint8_t *outs = nullptr;            // device block: status | sel | info | rew | done | agent
+  uint8_t *h_outs = nullptr;          // pinned host mirror of `outs`
   uint8_t *d_actions = nullptr;       // staging for host-provided actions
-  // pinned host views (lazy)
+  bool status_dirty = false;          // device status words may be non-zero
+};
+
+struct cog_env {
+  size_t n = 0;
+  std::vector<EnvShard> sh;
+  uint32_t *h_err = nullptr;          // pinned, device-mapped: one error word per shard (256 B apart)
+  // host views: obs is one pinned allocation; the small records are the shard's h_outs block
+  // when there is one shard, and batch-wide arrays gathered from the blocks otherwise
   bool host = false;
   cog_obs_t *h_obs = nullptr;
   cog_action_mask_t *h_sel = nullptr;
@@ -84,18 +128,22 @@ struct cog_env {
   uint8_t *h_done = nullptr;
   uint8_t *h_agent = nullptr;
   cog_info_t *h_info = nullptr;
-  uint32_t *h_status = nullptr;       // pinned [4]
   std::vector<uint32_t> dirty;
 };
 
-struct cog_sampler {
+struct SamplerShard {
   int device = 0;
+  size_t first = 0, n = 0;
   hipStream_t stream = nullptr;
-  size_t n = 0;
   uint32_t *d_rng = nullptr;
   uint8_t *d_actions = nullptr;
   uint8_t *d_masks = nullptr;         // staging for host-provided masks
-  cog_action_t *h_actions = nullptr;
+};
+
+struct cog_sampler {
+  size_t n = 0;
+  std::vector<SamplerShard> sh;
+  cog_action_t *h_actions = nullptr;  // persistent pinned view, all shards
 };
 
 struct cog_runner {
@@ -105,7 +153,7 @@ struct cog_runner {
   uint32_t flags = 0;
   bool pending_sample = false;
   bool timing = false;
-  std::vector<hipEvent_t> ev;         // pairs: one per step() launch or one per rollout() batch
+  std::vector<std::vector<hipEvent_t>> ev;   // per shard: pairs, one per step() launch or rollout() batch
   size_t ev_used = 0;
   uint64_t timed_launches = 0;        // fused launches covered by the recorded pairs
   int chunk = 1;                      // rollout steps per launch (>1: persistent K-step kernel)
@@ -113,100 +161,232 @@ struct cog_runner {
 
 namespace {
 
+bool single(const cog_env *e) { return e->sh.size() == 1; }
+
 void env_free(cog_env *e) {
   if (!e) return;
-  DeviceGuard g(e->device);
-  if (e->stream) (void)hipStreamSynchronize(e->stream);
-  void *dev[] = {e->s.obs, e->s.sel, e->s.info, e->s.rew, e->s.done, e->s.agent, e->s.priv,
-                 e->s.grid, e->s.cgrid, e->s.heads, e->s.park, e->s.gen, e->s.status, e->s.dirty, e->d_actions};
-  for (void *p : dev)
-    if (p) (void)hipFree(p);
-  void *hst[] = {e->h_obs, e->h_sel, e->h_rew, e->h_done, e->h_agent, e->h_info, e->h_status};
+  for (EnvShard &k : e->sh) {
+    DeviceGuard g(k.device);
+    if (k.stream) (void)hipStreamSynchronize(k.stream);
+    void *dev[] = {k.s.obs, k.outs, k.s.priv, k.s.grid, k.s.cgrid, k.s.heads, k.s.gen, k.s.dirty, k.d_actions};
+    for (void *p : dev)
+      if (p) (void)hipFree(p);
+    if (k.h_outs) (void)hipHostFree(k.h_outs);
+    if (k.ev) (void)hipEventDestroy(k.ev);
+    if (k.stream) (void)hipStreamDestroy(k.stream);
+  }
+  void *hst[] = {e->h_obs, e->h_err};
   for (void *p : hst)
     if (p) (void)hipHostFree(p);
-  if (e->stream) (void)hipStreamDestroy(e->stream);
+  if (!single(e)) {
+    void *more[] = {e->h_sel, e->h_rew, e->h_done, e->h_agent, e->h_info};
+    for (void *p : more)
+      if (p) (void)hipHostFree(p);
+  }
   delete e;
 }
 
-int read_status(cog_env *e, uint32_t out[4]) {
-  HIPCHK(hipMemcpyAsync(e->h_status, e->s.status, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(hipStreamSynchronize(e->stream));
-  std::memcpy(out, e->h_status, 4 * sizeof(uint32_t));
-  HIPCHK(hipMemsetAsync(e->s.status, 0, 4 * sizeof(uint32_t), e->stream));
+int sync_all(cog_env *e) {
+  for (EnvShard &k : e->sh) {
+    DeviceGuard g(k.device);
+    HIPCHK(hipStreamSynchronize(k.stream));
+  }
   return COG_OK;
 }
 
-int status_to_rc(const uint32_t st[4]) {
-  if (st[1]) {
-    if (st[0] & cog::F_GRID_OVER)
+int status_to_rc(uint32_t flags, uint32_t errors) {
+  if (errors) {
+    if (flags & cog::F_GRID_OVER)
       return fail(COG_ERR_MAPGEN, "map generation produced a map larger than the 48x48 observation grid");
     return fail(COG_ERR_MAPGEN, "Failed to generate map in specified maximum number of attempts");
   }
   return COG_OK;
 }
 
-// enqueue D2H of everything a step can change (obs dynamic tail, masks, outputs)
-int enqueue_refresh_tail(cog_env *e) {
-  const size_t n = e->s.n;
-  if (!n) return COG_OK;
-  HIPCHK(hipMemcpy2DAsync(reinterpret_cast<uint8_t *>(e->h_obs) + COG_OBS_MAP_BYTES, COG_OBS_BYTES,
-                          e->s.obs + COG_OBS_MAP_BYTES, COG_OBS_BYTES, COG_OBS_BYTES - COG_OBS_MAP_BYTES,
-                          n, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(hipMemcpyAsync(e->h_sel, e->s.sel, n * COG_MASK_BYTES, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(hipMemcpyAsync(e->h_rew, e->s.rew, n * 4 * sizeof(float), hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(hipMemcpyAsync(e->h_done, e->s.done, n, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(hipMemcpyAsync(e->h_agent, e->s.agent, n, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(hipMemcpyAsync(e->h_info, e->s.info, n * COG_INFO_BYTES, hipMemcpyDeviceToHost, e->stream));
+// the D2H copies a host-visible step needs: the ObsData tail (dynamic part: phase, resources,
+// shop, decks, stored masks) and the outs block (status words included)
+int enqueue_refresh(cog_env *e, EnvShard &k) {
+  if (!k.n) return COG_OK;
+  HIPCHK(hipMemcpy2DAsync(reinterpret_cast<uint8_t *>(e->h_obs + k.first) + COG_OBS_MAP_BYTES, COG_OBS_BYTES,
+                          k.s.obs + COG_OBS_MAP_BYTES, COG_OBS_BYTES, COG_OBS_BYTES - COG_OBS_MAP_BYTES, k.n,
+                          hipMemcpyDeviceToHost, k.stream));
+  HIPCHK(hipMemcpyAsync(k.h_outs, k.outs, OutLayout(k.n).total, hipMemcpyDeviceToHost, k.stream));
+  return COG_OK;
+}
+
+int enqueue_status_only(EnvShard &k) {
+  HIPCHK(hipMemcpyAsync(k.h_outs, k.outs, kStatusBytes, hipMemcpyDeviceToHost, k.stream));
+  return COG_OK;
+}
+
+// multi-shard handles keep batch-wide host arrays for the small records: gather the slices
+void gather_small(cog_env *e) {
+  if (single(e)) return;
+  for (EnvShard &k : e->sh) {
+    const OutLayout L(k.n);
+    std::memcpy(e->h_sel + k.first, k.h_outs + L.sel, k.n * COG_MASK_BYTES);
+    std::memcpy(e->h_info + k.first, k.h_outs + L.info, k.n * COG_INFO_BYTES);
+    std::memcpy(e->h_rew + 4 * k.first, k.h_outs + L.rew, k.n * 4 * sizeof(float));
+    std::memcpy(e->h_done + k.first, k.h_outs + L.done, k.n);
+    std::memcpy(e->h_agent + k.first, k.h_outs + L.agent, k.n);
+  }
+}
+
+// Status after a batch of work.  Device-only work (host views not refreshed) learns "no error"
+// from the host-mapped error words after the stream sync, with no copy; host-visible work reads
+// the status words that came with its refresh copy.  Regenerated maps (auto-resets) are copied
+// to the host views afterwards.  Status words are cleared only when they are non-zero.
+int finish(cog_env *e, bool refresh_host) {
+  const bool host = refresh_host && e->host;
+  for (EnvShard &k : e->sh) {
+    DeviceGuard g(k.device);
+    int rc = host ? enqueue_refresh(e, k) : COG_OK;
+    if (rc) return rc;
+  }
+  int rc = sync_all(e);
+  if (rc) return rc;
+  uint32_t flags = 0, errors = 0;
+  bool any_dirty = false;
+  for (size_t j = 0; j < e->sh.size(); j++) {
+    EnvShard &k = e->sh[j];
+    DeviceGuard g(k.device);
+    const bool err = e->h_err[64 * j] != 0u;
+    if (!host) {
+      if (!err) {
+        k.status_dirty = true;        // the dirty-map counter may have moved: clear before host use
+        continue;
+      }
+      if ((rc = enqueue_status_only(k))) return rc;
+      HIPCHK(hipStreamSynchronize(k.stream));
+    }
+    const uint32_t *st = reinterpret_cast<const uint32_t *>(k.h_outs);
+    const uint32_t st0 = st[0], st1 = st[1], st2 = st[2];
+    flags |= st0;
+    errors += st1;
+    if (host && st2) {
+      any_dirty = true;
+      if (st2 >= k.n / 8 || st2 > k.s.cap) {   // many resets (or list overflow): copy every map
+        HIPCHK(hipMemcpy2DAsync(e->h_obs + k.first, COG_OBS_BYTES, k.s.obs, COG_OBS_BYTES, COG_OBS_MAP_BYTES, k.n,
+                                hipMemcpyDeviceToHost, k.stream));
+      } else {
+        e->dirty.resize(st2);
+        HIPCHK(hipMemcpyAsync(e->dirty.data(), k.s.dirty, st2 * sizeof(uint32_t), hipMemcpyDeviceToHost, k.stream));
+        HIPCHK(hipStreamSynchronize(k.stream));
+        for (uint32_t q = 0; q < st2; q++) {
+          const size_t i = e->dirty[q];
+          HIPCHK(hipMemcpyAsync(reinterpret_cast<uint8_t *>(e->h_obs + k.first + i), k.s.obs + i * COG_OBS_BYTES,
+                                COG_OBS_MAP_BYTES, hipMemcpyDeviceToHost, k.stream));
+        }
+      }
+    }
+    if (st0 || st1 || st2 || k.status_dirty || err) {
+      HIPCHK(hipMemsetAsync(k.outs, 0, kStatusBytes, k.stream));
+      e->h_err[64 * j] = 0u;
+      k.status_dirty = false;
+    }
+  }
+  if (any_dirty && (rc = sync_all(e))) return rc;
+  if (host) gather_small(e);
+  return status_to_rc(flags, errors);
+}
+
+// before a host-visible batch: status words still counting from device-only work are cleared
+int prepare_host(cog_env *e) {
+  for (EnvShard &k : e->sh) {
+    if (!k.status_dirty) continue;
+    DeviceGuard g(k.device);
+    HIPCHK(hipMemsetAsync(k.outs, 0, kStatusBytes, k.stream));
+    k.status_dirty = false;
+  }
   return COG_OK;
 }
 
 int refresh_full(cog_env *e) {
-  if (!e->host || !e->s.n) return COG_OK;
-  HIPCHK(hipMemcpyAsync(e->h_obs, e->s.obs, e->s.n * COG_OBS_BYTES, hipMemcpyDeviceToHost, e->stream));
-  int rc = enqueue_refresh_tail(e);
+  if (!e->host || !e->n) return COG_OK;
+  for (EnvShard &k : e->sh) {
+    if (!k.n) continue;
+    DeviceGuard g(k.device);
+    HIPCHK(hipMemcpyAsync(e->h_obs + k.first, k.s.obs, k.n * COG_OBS_BYTES, hipMemcpyDeviceToHost, k.stream));
+    HIPCHK(hipMemcpyAsync(k.h_outs + kStatusBytes, k.outs + kStatusBytes, OutLayout(k.n).total - kStatusBytes,
+                          hipMemcpyDeviceToHost, k.stream));
+  }
+  int rc = sync_all(e);
   if (rc) return rc;
-  HIPCHK(hipStreamSynchronize(e->stream));
+  gather_small(e);
   return COG_OK;
 }
 
-// after steps: status word + dynamic tail, then the maps of re-generated envs
-int finish_steps(cog_env *e, bool refresh_host) {
-  if (refresh_host && e->host) {
-    int rc = enqueue_refresh_tail(e);
-    if (rc) return rc;
-  }
-  uint32_t st[4];
-  int rc = read_status(e, st);
-  if (rc) return rc;
-  const uint32_t ndirty = st[2];
-  if (refresh_host && e->host && ndirty) {
-    if (ndirty >= e->s.n / 8) {   // many resets (or list overflow): copy every map
-      HIPCHK(hipMemcpy2DAsync(e->h_obs, COG_OBS_BYTES, e->s.obs, COG_OBS_BYTES, COG_OBS_MAP_BYTES, e->s.n,
-                              hipMemcpyDeviceToHost, e->stream));
-    } else {
-      e->dirty.resize(ndirty);
-      HIPCHK(hipMemcpy(e->dirty.data(), e->s.dirty, ndirty * sizeof(uint32_t), hipMemcpyDeviceToHost));
-      for (uint32_t k = 0; k < ndirty; k++) {
-        const size_t i = e->dirty[k];
-        HIPCHK(hipMemcpyAsync(reinterpret_cast<uint8_t *>(e->h_obs) + i * COG_OBS_BYTES,
-                              e->s.obs + i * COG_OBS_BYTES, COG_OBS_MAP_BYTES, hipMemcpyDeviceToHost, e->stream));
-      }
-    }
-    HIPCHK(hipStreamSynchronize(e->stream));
-  }
-  return status_to_rc(st);
+// the shard's state as the kernels see it: no dirty-map list unless the host views follow
+cog::DevState launch_state(const EnvShard &k, bool host_views) {
+  cog::DevState s = k.s;
+  if (!host_views) s.cap = 0;
+  return s;
 }
 
 void sampler_free(cog_sampler *s) {
   if (!s) return;
-  DeviceGuard g(s->device);
-  if (s->stream) (void)hipStreamSynchronize(s->stream);
-  void *dev[] = {s->d_rng, s->d_actions, s->d_masks};
-  for (void *p : dev)
-    if (p) (void)hipFree(p);
+  for (SamplerShard &k : s->sh) {
+    DeviceGuard g(k.device);
+    if (k.stream) (void)hipStreamSynchronize(k.stream);
+    void *dev[] = {k.d_rng, k.d_actions, k.d_masks};
+    for (void *p : dev)
+      if (p) (void)hipFree(p);
+    if (k.stream) (void)hipStreamDestroy(k.stream);
+  }
   if (s->h_actions) (void)hipHostFree(s->h_actions);
-  if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
+}
+
+int check_devices(const int *devices, int n_devices) {
+  if (!devices || n_devices < 1) return fail(COG_ERR_INVALID, "need at least one device");
+  for (int j = 0; j < n_devices; j++) {
+    int rc = check_device(devices[j]);
+    if (rc) return rc;
+  }
+  return COG_OK;
+}
+
+int env_shard_init(EnvShard &k, uint32_t default_seed, uint32_t *err_word) {
+  DeviceGuard g(k.device);
+  HIPCHK(hipStreamCreateWithFlags(&k.stream, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&k.ev, hipEventDisableTiming));
+  const size_t n = k.n;
+  const OutLayout L(n);
+  cog::DevState &s = k.s;
+  int rc;
+  if ((rc = dmalloc(&s.obs, n * COG_OBS_BYTES)) || (rc = dmalloc(&k.outs, L.total)) ||
+      (rc = dmalloc(&s.priv, n * sizeof(cog::EnvPriv))) || (rc = dmalloc(&s.grid, n * (size_t)cog::kGridBytes)) ||
+      (rc = dmalloc(&s.cgrid, n * (size_t)COG_CELLS)) || (rc = dmalloc(&s.heads, n * 5 * sizeof(uint4))) ||
+      (rc = dmalloc(&s.gen, n * sizeof(cog::GenScratch))) || (rc = dmalloc(&s.dirty, n * sizeof(uint32_t))) ||
+      (rc = dmalloc(&k.d_actions, n * COG_ACTION_BYTES)) || (rc = hmalloc(&k.h_outs, L.total)))
+    return rc;
+  std::memset(k.h_outs, 0, L.total);
+  s.n = n;
+  s.first = k.first;
+  s.cap = n;
+  s.autoreset = 1;
+  s.status = reinterpret_cast<uint32_t *>(k.outs);
+  s.sel = k.outs + L.sel;
+  s.info = k.outs + L.info;
+  s.rew = reinterpret_cast<float *>(k.outs + L.rew);
+  s.done = k.outs + L.done;
+  s.agent = k.outs + L.agent;
+  void *d_err = nullptr;
+  HIPCHK(hipHostGetDevicePointer(&d_err, err_word, 0));
+  s.err = static_cast<uint32_t *>(d_err);
+  struct { void *p; size_t b; } z[] = {{s.obs, n * COG_OBS_BYTES}, {k.outs, L.total}, {s.grid, n * (size_t)cog::kGridBytes},
+                                       {s.cgrid, n * (size_t)COG_CELLS}, {s.gen, n * sizeof(cog::GenScratch)},
+                                       {k.d_actions, n * COG_ACTION_BYTES}};
+  for (auto &zz : z)
+    if (zz.b) HIPCHK(hipMemsetAsync(zz.p, 0, zz.b, k.stream));
+  if (cog::launch_init(s, nullptr, default_seed, k.stream))
+    return fail(COG_ERR_HIP, std::string("env init kernel failed: ") + hipGetErrorString(hipGetLastError()));
+  return COG_OK;
+}
+
+int shard_of(const cog_env *e, int k) {
+  if (!e || k < 0 || (size_t)k >= e->sh.size()) return fail(COG_ERR_INVALID, "shard index out of range");
+  return COG_OK;
 }
 
 }  // namespace
@@ -224,77 +404,90 @@ int cog_device_count(int *out) {
   return COG_OK;
 }
 
-int cog_env_create(size_t n_envs, int device, cog_env **out) {
+int cog_env_create_multi(size_t n_envs, const int *devices, int n_devices, cog_env **out) {
   if (!out) return fail(COG_ERR_INVALID, "out is NULL");
   *out = nullptr;
-  int rc = check_device(device);
+  int rc = check_devices(devices, n_devices);
   if (rc) return rc;
-  DeviceGuard g(device);
   cog_env *e = new cog_env();
-  e->device = device;
-  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
-    env_free(e);
-    return fail(COG_ERR_HIP, "hipStreamCreate failed");
-  }
-  const size_t n = n_envs;
-  cog::DevState &s = e->s;
-  s.n = n;
-  s.first = 0;
-  s.cap = n;
-  s.autoreset = 1;
-  if ((rc = dmalloc(&s.obs, n * COG_OBS_BYTES)) || (rc = dmalloc(&s.sel, n * COG_MASK_BYTES)) ||
-      (rc = dmalloc(&s.info, n * COG_INFO_BYTES)) || (rc = dmalloc(&s.rew, n * 4 * sizeof(float))) ||
-      (rc = dmalloc(&s.done, n)) || (rc = dmalloc(&s.agent, n)) ||
-      (rc = dmalloc(&s.priv, n * sizeof(cog::EnvPriv))) ||
-      (rc = dmalloc(&s.grid, n * (size_t)cog::kGridBytes)) || (rc = dmalloc(&s.cgrid, n * (size_t)COG_CELLS)) ||
-      (rc = dmalloc(&s.heads, n * 5 * sizeof(uint4))) || (rc = dmalloc(&s.park, n * sizeof(uint32_t))) ||
-      (rc = dmalloc(&s.gen, n * sizeof(cog::GenScratch))) || (rc = dmalloc(&s.status, 64)) ||
-      (rc = dmalloc(&s.dirty, n * sizeof(uint32_t))) || (rc = dmalloc(&e->d_actions, n * COG_ACTION_BYTES)) ||
-      (rc = hmalloc(&e->h_status, 64))) {
+  e->n = n_envs;
+  const size_t err_bytes = 64 * sizeof(uint32_t) * (size_t)n_devices;
+  if ((rc = hmalloc(&e->h_err, err_bytes, hipHostMallocMapped | hipHostMallocCoherent))) {
     env_free(e);
     return rc;
   }
-  struct { void *p; size_t b; } z[] = {
-      {s.obs, n * COG_OBS_BYTES}, {s.sel, n * COG_MASK_BYTES}, {s.info, n * COG_INFO_BYTES},
-      {s.rew, n * 4 * sizeof(float)}, {s.done, n}, {s.agent, n}, {s.grid, n * (size_t)cog::kGridBytes},
-      {s.cgrid, n * (size_t)COG_CELLS},
-      {s.gen, n * sizeof(cog::GenScratch)}, {s.status, 64}, {e->d_actions, n * COG_ACTION_BYTES}};
-  for (auto &zz : z)
-    if (zz.b && hipMemsetAsync(zz.p, 0, zz.b, e->stream) != hipSuccess) {
-      env_free(e);
-      return fail(COG_ERR_HIP, "hipMemsetAsync failed");
-    }
-  if (hipMemsetAsync(s.park, 0xff, n * sizeof(uint32_t), e->stream) != hipSuccess) {   // nothing parked
-    env_free(e);
-    return fail(COG_ERR_HIP, "hipMemsetAsync failed");
-  }
+  std::memset(e->h_err, 0, err_bytes);
+  const std::vector<size_t> first = block_split(n_envs, n_devices);
   const uint32_t default_seed = std::random_device{}();   // cog_env() seeds from random_device
-  if (cog::launch_init(s, nullptr, default_seed, e->stream) || hipStreamSynchronize(e->stream) != hipSuccess) {
+  e->sh.resize(n_devices);
+  for (int j = 0; j < n_devices; j++) {
+    EnvShard &k = e->sh[j];
+    k.device = devices[j];
+    k.first = first[j];
+    k.n = first[j + 1] - first[j];
+    if ((rc = env_shard_init(k, default_seed, e->h_err + 64 * j))) {   // one 256-B line per shard
+      env_free(e);
+      return rc;
+    }
+  }
+  if ((rc = sync_all(e))) {
     env_free(e);
-    return fail(COG_ERR_HIP, std::string("env init kernel failed: ") + hipGetErrorString(hipGetLastError()));
+    return rc;
   }
   *out = e;
   return COG_OK;
 }
 
+int cog_env_create(size_t n_envs, int device, cog_env **out) { return cog_env_create_multi(n_envs, &device, 1, out); }
+
 void cog_env_destroy(cog_env *env) { env_free(env); }
 
 int cog_env_num_envs(const cog_env *env, size_t *out) {
   if (!env || !out) return fail(COG_ERR_INVALID, "NULL argument");
-  *out = env->s.n;
+  *out = env->n;
+  return COG_OK;
+}
+
+int cog_env_num_shards(const cog_env *env, int *out) {
+  if (!env || !out) return fail(COG_ERR_INVALID, "NULL argument");
+  *out = (int)env->sh.size();
+  return COG_OK;
+}
+
+int cog_env_shard_info(const cog_env *env, int k, size_t *first, size_t *count, int *device) {
+  int rc = shard_of(env, k);
+  if (rc) return rc;
+  const EnvShard &s = env->sh[k];
+  if (first) *first = s.first;
+  if (count) *count = s.n;
+  if (device) *device = s.device;
   return COG_OK;
 }
 
 static int env_reset_impl(cog_env *e, const cog::ResetParams &p) {
-  DeviceGuard g(e->device);
-  if (cog::launch_reset(e->s, p, e->stream) || cog::launch_encode_all(e->s, e->stream))
-    return fail(COG_ERR_HIP, std::string("reset launch failed: ") + hipGetErrorString(hipGetLastError()));
-  uint32_t st[4];
-  int rc = read_status(e, st);
+  int rc = prepare_host(e);
   if (rc) return rc;
-  rc = refresh_full(e);
-  if (rc) return rc;
-  return status_to_rc(st);
+  for (EnvShard &k : e->sh) {
+    DeviceGuard g(k.device);
+    if (cog::launch_reset(k.s, p, k.stream) || cog::launch_encode_all(k.s, k.stream))
+      return fail(COG_ERR_HIP, std::string("reset launch failed: ") + hipGetErrorString(hipGetLastError()));
+    if ((rc = enqueue_status_only(k))) return rc;
+  }
+  if ((rc = sync_all(e))) return rc;
+  uint32_t flags = 0, errors = 0;
+  for (size_t j = 0; j < e->sh.size(); j++) {
+    EnvShard &k = e->sh[j];
+    const uint32_t *st = reinterpret_cast<const uint32_t *>(k.h_outs);
+    flags |= st[0];
+    errors += st[1];
+    if (st[0] || st[1] || st[2] || e->h_err[64 * j]) {
+      DeviceGuard g(k.device);
+      HIPCHK(hipMemsetAsync(k.outs, 0, kStatusBytes, k.stream));
+      e->h_err[64 * j] = 0u;
+    }
+  }
+  if ((rc = refresh_full(e))) return rc;
+  return status_to_rc(flags, errors);
 }
 
 int cog_env_reset(cog_env *env, uint32_t seed, uint8_t n_players, uint8_t n_pieces, int32_t difficulty,
@@ -314,68 +507,132 @@ int cog_env_reset_default(cog_env *env) {
   return env_reset_impl(env, p);
 }
 
-int cog_env_step_device(cog_env *env, const void *d_actions, size_t n) {
+int cog_env_step_device_stream(cog_env *env, const void *d_actions, size_t n, void *stream) {
   if (!env || !d_actions) return fail(COG_ERR_INVALID, "NULL argument");
-  if (n != env->s.n) return fail(COG_ERR_INVALID, "actions length != num_envs");
-  DeviceGuard g(env->device);
-  if (cog::launch_step(env->s, static_cast<const uint8_t *>(d_actions), env->stream))
+  if (n != env->n) return fail(COG_ERR_INVALID, "actions length != num_envs");
+  if (!single(env)) return fail(COG_ERR_INVALID, "device actions need a single-shard env (one device pointer)");
+  EnvShard &k = env->sh[0];
+  DeviceGuard g(k.device);
+  int rc = prepare_host(env);
+  if (rc) return rc;
+  if (stream) {                       // the caller's stream produced the actions: order after it
+    HIPCHK(hipEventRecord(k.ev, static_cast<hipStream_t>(stream)));
+    HIPCHK(hipStreamWaitEvent(k.stream, k.ev, 0));
+  }
+  if (cog::launch_step(launch_state(k, env->host), static_cast<const uint8_t *>(d_actions), k.stream))
     return fail(COG_ERR_HIP, std::string("step launch failed: ") + hipGetErrorString(hipGetLastError()));
-  return finish_steps(env, true);
+  return finish(env, true);
+}
+
+int cog_env_step_device(cog_env *env, const void *d_actions, size_t n) {
+  return cog_env_step_device_stream(env, d_actions, n, nullptr);
 }
 
 int cog_env_step(cog_env *env, const cog_action_t *actions, size_t n) {
   if (!env || (!actions && n)) return fail(COG_ERR_INVALID, "NULL argument");
-  if (n != env->s.n) return fail(COG_ERR_INVALID, "actions length != num_envs");
-  DeviceGuard g(env->device);
-  if (n) HIPCHK(hipMemcpyAsync(env->d_actions, actions, n * COG_ACTION_BYTES, hipMemcpyHostToDevice, env->stream));
-  return cog_env_step_device(env, env->d_actions, n);
+  if (n != env->n) return fail(COG_ERR_INVALID, "actions length != num_envs");
+  int rc = prepare_host(env);
+  if (rc) return rc;
+  for (EnvShard &k : env->sh) {
+    if (!k.n) continue;
+    DeviceGuard g(k.device);
+    HIPCHK(hipMemcpyAsync(k.d_actions, actions + k.first, k.n * COG_ACTION_BYTES, hipMemcpyHostToDevice, k.stream));
+    if (cog::launch_step(launch_state(k, env->host), k.d_actions, k.stream))
+      return fail(COG_ERR_HIP, std::string("step launch failed: ") + hipGetErrorString(hipGetLastError()));
+  }
+  return finish(env, true);
+}
+
+static int alloc_host_views(cog_env *env) {
+  const size_t n = env->n;
+  int rc;
+  if ((rc = hmalloc(&env->h_obs, n * COG_OBS_BYTES))) return rc;
+  std::memset(env->h_obs, 0, n * COG_OBS_BYTES);   // padding bytes stay defined
+  if (single(env)) {                                // views point straight into the copy target
+    EnvShard &k = env->sh[0];
+    const OutLayout L(k.n);
+    env->h_sel = reinterpret_cast<cog_action_mask_t *>(k.h_outs + L.sel);
+    env->h_info = reinterpret_cast<cog_info_t *>(k.h_outs + L.info);
+    env->h_rew = reinterpret_cast<float *>(k.h_outs + L.rew);
+    env->h_done = k.h_outs + L.done;
+    env->h_agent = k.h_outs + L.agent;
+  } else if ((rc = hmalloc(&env->h_sel, n * COG_MASK_BYTES)) || (rc = hmalloc(&env->h_rew, n * 4 * sizeof(float))) ||
+             (rc = hmalloc(&env->h_done, n)) || (rc = hmalloc(&env->h_agent, n)) ||
+             (rc = hmalloc(&env->h_info, n * COG_INFO_BYTES))) {
+    return rc;
+  }
+  env->host = true;
+  return refresh_full(env);
 }
 
 int cog_env_get_views(cog_env *env, cog_env_views *out) {
   if (!env || !out) return fail(COG_ERR_INVALID, "NULL argument");
-  DeviceGuard g(env->device);
   if (!env->host) {
-    const size_t n = env->s.n;
-    int rc;
-    if ((rc = hmalloc(&env->h_obs, n * COG_OBS_BYTES)) || (rc = hmalloc(&env->h_sel, n * COG_MASK_BYTES)) ||
-        (rc = hmalloc(&env->h_rew, n * 4 * sizeof(float))) || (rc = hmalloc(&env->h_done, n)) ||
-        (rc = hmalloc(&env->h_agent, n)) || (rc = hmalloc(&env->h_info, n * COG_INFO_BYTES)))
-      return rc;
-    std::memset(env->h_obs, 0, n * COG_OBS_BYTES);   // padding bytes stay defined
-    env->host = true;
-    rc = refresh_full(env);
+    int rc = alloc_host_views(env);
     if (rc) return rc;
   }
-  out->n_envs = env->s.n;
+  std::memset(out, 0, sizeof(*out));
+  out->n_envs = env->n;
   out->observations = env->h_obs;
   out->selected_action_masks = env->h_sel;
   out->rewards = env->h_rew;
   out->dones = env->h_done;
   out->agent_selection = env->h_agent;
   out->infos = env->h_info;
-  out->d_observations = env->s.obs;
-  out->d_selected_action_masks = env->s.sel;
-  out->d_rewards = env->s.rew;
-  out->d_dones = env->s.done;
-  out->d_agent_selection = env->s.agent;
-  out->d_infos = env->s.info;
+  if (single(env)) {                                // device views: one device pointer per record kind
+    const EnvShard &k = env->sh[0];
+    out->d_observations = k.s.obs;
+    out->d_selected_action_masks = k.s.sel;
+    out->d_rewards = k.s.rew;
+    out->d_dones = k.s.done;
+    out->d_agent_selection = k.s.agent;
+    out->d_infos = k.s.info;
+  }
+  return COG_OK;
+}
+
+int cog_env_shard_views(cog_env *env, int k, cog_env_views *out) {
+  int rc = shard_of(env, k);
+  if (rc) return rc;
+  if (!out) return fail(COG_ERR_INVALID, "NULL argument");
+  cog_env_views all;
+  if ((rc = cog_env_get_views(env, &all))) return rc;
+  const EnvShard &s = env->sh[k];
+  std::memset(out, 0, sizeof(*out));
+  out->n_envs = s.n;
+  out->observations = all.observations + s.first;
+  out->selected_action_masks = all.selected_action_masks + s.first;
+  out->rewards = all.rewards + 4 * s.first;
+  out->dones = all.dones + s.first;
+  out->agent_selection = all.agent_selection + s.first;
+  out->infos = all.infos + s.first;
+  out->d_observations = s.s.obs;
+  out->d_selected_action_masks = s.s.sel;
+  out->d_rewards = s.s.rew;
+  out->d_dones = s.s.done;
+  out->d_agent_selection = s.s.agent;
+  out->d_infos = s.s.info;
   return COG_OK;
 }
 
 int cog_env_sync_host(cog_env *env) {
   if (!env) return fail(COG_ERR_INVALID, "env is NULL");
-  DeviceGuard g(env->device);
+  if (!env->host) return alloc_host_views(env);
   return refresh_full(env);
 }
 
 int cog_env_hazards(cog_env *env, uint32_t *flags_or, uint32_t *per_env) {
   if (!env) return fail(COG_ERR_INVALID, "env is NULL");
-  DeviceGuard g(env->device);
-  std::vector<uint32_t> tmp(env->s.n);
-  if (env->s.n)
-    HIPCHK(hipMemcpy2DAsync(tmp.data(), sizeof(uint32_t), reinterpret_cast<uint8_t *>(env->s.priv) + offsetof(cog::EnvPriv, flags),
-                            sizeof(cog::EnvPriv), sizeof(uint32_t), env->s.n, hipMemcpyDeviceToHost, env->stream));
-  HIPCHK(hipStreamSynchronize(env->stream));
+  std::vector<uint32_t> tmp(env->n);
+  for (EnvShard &k : env->sh) {
+    if (!k.n) continue;
+    DeviceGuard g(k.device);
+    HIPCHK(hipMemcpy2DAsync(tmp.data() + k.first, sizeof(uint32_t),
+                            reinterpret_cast<uint8_t *>(k.s.priv) + offsetof(cog::EnvPriv, flags), sizeof(cog::EnvPriv),
+                            sizeof(uint32_t), k.n, hipMemcpyDeviceToHost, k.stream));
+  }
+  int rc = sync_all(env);
+  if (rc) return rc;
   uint32_t acc = 0;
   for (uint32_t f : tmp) acc |= f;
   if (flags_or) *flags_or = acc;
@@ -385,26 +642,28 @@ int cog_env_hazards(cog_env *env, uint32_t *flags_or, uint32_t *per_env) {
 
 int cog_env_clear_hazards(cog_env *env) {
   if (!env) return fail(COG_ERR_INVALID, "env is NULL");
-  DeviceGuard g(env->device);
-  if (env->s.n)
-    HIPCHK(hipMemset2DAsync(reinterpret_cast<uint8_t *>(env->s.priv) + offsetof(cog::EnvPriv, flags), sizeof(cog::EnvPriv),
-                            0, sizeof(uint32_t), env->s.n, env->stream));
-  HIPCHK(hipStreamSynchronize(env->stream));
-  return COG_OK;
+  for (EnvShard &k : env->sh) {
+    if (!k.n) continue;
+    DeviceGuard g(k.device);
+    HIPCHK(hipMemset2DAsync(reinterpret_cast<uint8_t *>(k.s.priv) + offsetof(cog::EnvPriv, flags), sizeof(cog::EnvPriv),
+                            0, sizeof(uint32_t), k.n, k.stream));
+  }
+  return sync_all(env);
 }
 
 int cog_env_time_encode(cog_env *env, int iters, int variant, double *ms_per_launch) {
   if (!env || iters < 1 || !ms_per_launch) return fail(COG_ERR_INVALID, "bad argument");
-  DeviceGuard g(env->device);
+  EnvShard &k = env->sh[0];                         // diagnostic: shard 0
+  DeviceGuard g(k.device);
   hipEvent_t e0, e1;
   HIPCHK(hipEventCreate(&e0));
   HIPCHK(hipEventCreate(&e1));
-  if (cog::launch_encode_all(env->s, env->stream, variant))   // warm-up launch
+  if (cog::launch_encode_all(k.s, k.stream, variant))   // warm-up launch
     return fail(COG_ERR_HIP, "encode launch failed");
-  HIPCHK(hipEventRecord(e0, env->stream));
-  for (int k = 0; k < iters; k++)
-    if (cog::launch_encode_all(env->s, env->stream, variant)) return fail(COG_ERR_HIP, "encode launch failed");
-  HIPCHK(hipEventRecord(e1, env->stream));
+  HIPCHK(hipEventRecord(e0, k.stream));
+  for (int r = 0; r < iters; r++)
+    if (cog::launch_encode_all(k.s, k.stream, variant)) return fail(COG_ERR_HIP, "encode launch failed");
+  HIPCHK(hipEventRecord(e1, k.stream));
   HIPCHK(hipEventSynchronize(e1));
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, e0, e1));
@@ -414,88 +673,161 @@ int cog_env_time_encode(cog_env *env, int iters, int variant, double *ms_per_lau
   return COG_OK;
 }
 
-void *cog_env_stream(cog_env *env) { return env ? (void *)env->stream : nullptr; }
-int cog_env_device(const cog_env *env) { return env ? env->device : -1; }
-int cog_env_set_autoreset(cog_env *env, int on) {
-  if (!env) return fail(COG_ERR_INVALID, "env is NULL");
-  DeviceGuard g(env->device);
-  if (hipStreamSynchronize(env->stream) != hipSuccess) return fail(COG_ERR_HIP, "hipStreamSynchronize failed");
-  env->s.autoreset = on ? 1u : 0u;
+void *cog_env_stream(cog_env *env) { return env ? (void *)env->sh[0].stream : nullptr; }
+void *cog_env_shard_stream(cog_env *env, int k) {
+  if (!env || k < 0 || (size_t)k >= env->sh.size()) return nullptr;
+  return (void *)env->sh[k].stream;
+}
+int cog_env_device(const cog_env *env) { return env ? env->sh[0].device : -1; }
+
+int cog_env_wait_stream(cog_env *env, int k, void *stream) {
+  int rc = shard_of(env, k);
+  if (rc) return rc;
+  EnvShard &s = env->sh[k];
+  DeviceGuard g(s.device);
+  HIPCHK(hipEventRecord(s.ev, static_cast<hipStream_t>(stream)));
+  HIPCHK(hipStreamWaitEvent(s.stream, s.ev, 0));
   return COG_OK;
 }
-int cog_sampler_device(const cog_sampler *s) { return s ? s->device : -1; }
+
+int cog_env_signal_stream(cog_env *env, int k, void *stream) {
+  int rc = shard_of(env, k);
+  if (rc) return rc;
+  EnvShard &s = env->sh[k];
+  DeviceGuard g(s.device);
+  HIPCHK(hipEventRecord(s.ev, s.stream));
+  HIPCHK(hipStreamWaitEvent(static_cast<hipStream_t>(stream), s.ev, 0));
+  return COG_OK;
+}
+
+int cog_env_set_autoreset(cog_env *env, int on) {
+  if (!env) return fail(COG_ERR_INVALID, "env is NULL");
+  int rc = sync_all(env);
+  if (rc) return rc;
+  for (EnvShard &k : env->sh) k.s.autoreset = on ? 1u : 0u;
+  return COG_OK;
+}
 
 // ---- sampler -----------------------------------------------------------------------------
-int cog_sampler_create(size_t n_envs, uint64_t seed, int device, cog_sampler **out) {
+int cog_sampler_create_multi(size_t n_envs, uint64_t seed, const int *devices, int n_devices, cog_sampler **out) {
   if (!out) return fail(COG_ERR_INVALID, "out is NULL");
   *out = nullptr;
-  int rc = check_device(device);
+  int rc = check_devices(devices, n_devices);
   if (rc) return rc;
-  DeviceGuard g(device);
   cog_sampler *s = new cog_sampler();
-  s->device = device;
   s->n = n_envs;
-  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
-    sampler_free(s);
-    return fail(COG_ERR_HIP, "hipStreamCreate failed");
-  }
-  if ((rc = dmalloc(&s->d_rng, n_envs * sizeof(uint32_t))) || (rc = dmalloc(&s->d_actions, n_envs * COG_ACTION_BYTES)) ||
-      (rc = dmalloc(&s->d_masks, n_envs * COG_MASK_BYTES)) || (rc = hmalloc(&s->h_actions, n_envs * COG_ACTION_BYTES))) {
+  if ((rc = hmalloc(&s->h_actions, n_envs * COG_ACTION_BYTES))) {
     sampler_free(s);
     return rc;
   }
   std::memset(s->h_actions, 0, n_envs * COG_ACTION_BYTES);
-  if (hipMemsetAsync(s->d_actions, 0, n_envs * COG_ACTION_BYTES, s->stream) != hipSuccess ||
-      cog::launch_seed_sampler(n_envs, (uint32_t)seed, s->d_rng, s->stream) ||
-      hipStreamSynchronize(s->stream) != hipSuccess) {
-    sampler_free(s);
-    return fail(COG_ERR_HIP, "sampler init failed");
+  const std::vector<size_t> first = block_split(n_envs, n_devices);
+  s->sh.resize(n_devices);
+  for (int j = 0; j < n_devices; j++) {
+    SamplerShard &k = s->sh[j];
+    k.device = devices[j];
+    k.first = first[j];
+    k.n = first[j + 1] - first[j];
+    DeviceGuard g(k.device);
+    if (hipStreamCreateWithFlags(&k.stream, hipStreamNonBlocking) != hipSuccess) {
+      sampler_free(s);
+      return fail(COG_ERR_HIP, "hipStreamCreate failed");
+    }
+    if ((rc = dmalloc(&k.d_rng, k.n * sizeof(uint32_t))) || (rc = dmalloc(&k.d_actions, k.n * COG_ACTION_BYTES)) ||
+        (rc = dmalloc(&k.d_masks, k.n * COG_MASK_BYTES))) {
+      sampler_free(s);
+      return rc;
+    }
+    // vec_action_sampler(seed) (vec_sampler.h:9-13): sampler i seeded seed + i, seed a u32
+    if (hipMemsetAsync(k.d_actions, 0, k.n * COG_ACTION_BYTES, k.stream) != hipSuccess ||
+        cog::launch_seed_sampler(k.n, (uint64_t)(uint32_t)seed, k.first, k.d_rng, k.stream)) {
+      sampler_free(s);
+      return fail(COG_ERR_HIP, "sampler init failed");
+    }
+  }
+  for (SamplerShard &k : s->sh) {
+    DeviceGuard g(k.device);
+    if (hipStreamSynchronize(k.stream) != hipSuccess) {
+      sampler_free(s);
+      return fail(COG_ERR_HIP, "sampler init failed");
+    }
   }
   *out = s;
   return COG_OK;
 }
 
+int cog_sampler_create(size_t n_envs, uint64_t seed, int device, cog_sampler **out) {
+  return cog_sampler_create_multi(n_envs, seed, &device, 1, out);
+}
+
 void cog_sampler_destroy(cog_sampler *s) { sampler_free(s); }
 
-static int sampler_run(cog_sampler *s, const uint8_t *d_masks, hipStream_t stream, bool host_refresh) {
-  if (cog::launch_sample(s->n, d_masks, s->d_rng, s->d_actions, stream))
+int cog_sampler_num_shards(const cog_sampler *s, int *out) {
+  if (!s || !out) return fail(COG_ERR_INVALID, "NULL argument");
+  *out = (int)s->sh.size();
+  return COG_OK;
+}
+
+static int sampler_run(SamplerShard &k, cog_action_t *h_actions, const uint8_t *d_masks, hipStream_t stream,
+                       bool host_refresh) {
+  if (cog::launch_sample(k.n, d_masks, k.d_rng, k.d_actions, stream))
     return fail(COG_ERR_HIP, std::string("sample launch failed: ") + hipGetErrorString(hipGetLastError()));
-  if (host_refresh && s->n)
-    HIPCHK(hipMemcpyAsync(s->h_actions, s->d_actions, s->n * COG_ACTION_BYTES, hipMemcpyDeviceToHost, stream));
+  if (host_refresh && k.n)
+    HIPCHK(hipMemcpyAsync(h_actions + k.first, k.d_actions, k.n * COG_ACTION_BYTES, hipMemcpyDeviceToHost, stream));
   return COG_OK;
 }
 
 int cog_sampler_sample_device(cog_sampler *s, const void *d_masks, size_t n) {
   if (!s || !d_masks) return fail(COG_ERR_INVALID, "NULL argument");
   if (n != s->n) return fail(COG_ERR_INVALID, "action_mask length != num_envs");
-  DeviceGuard g(s->device);
-  int rc = sampler_run(s, static_cast<const uint8_t *>(d_masks), s->stream, true);
+  if (s->sh.size() != 1) return fail(COG_ERR_INVALID, "device masks need a single-shard sampler (one device pointer)");
+  SamplerShard &k = s->sh[0];
+  DeviceGuard g(k.device);
+  int rc = sampler_run(k, s->h_actions, static_cast<const uint8_t *>(d_masks), k.stream, true);
   if (rc) return rc;
-  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(hipStreamSynchronize(k.stream));
   return COG_OK;
 }
 
 int cog_sampler_sample(cog_sampler *s, const cog_action_mask_t *masks, size_t n) {
   if (!s || (!masks && n)) return fail(COG_ERR_INVALID, "NULL argument");
   if (n != s->n) return fail(COG_ERR_INVALID, "action_mask length != num_envs");
-  DeviceGuard g(s->device);
-  if (n) HIPCHK(hipMemcpyAsync(s->d_masks, masks, n * COG_MASK_BYTES, hipMemcpyHostToDevice, s->stream));
-  return cog_sampler_sample_device(s, s->d_masks, n);
+  for (SamplerShard &k : s->sh) {
+    if (!k.n) continue;
+    DeviceGuard g(k.device);
+    HIPCHK(hipMemcpyAsync(k.d_masks, masks + k.first, k.n * COG_MASK_BYTES, hipMemcpyHostToDevice, k.stream));
+    int rc = sampler_run(k, s->h_actions, k.d_masks, k.stream, true);
+    if (rc) return rc;
+  }
+  for (SamplerShard &k : s->sh) {
+    DeviceGuard g(k.device);
+    HIPCHK(hipStreamSynchronize(k.stream));
+  }
+  return COG_OK;
 }
 
 cog_action_t *cog_sampler_actions(cog_sampler *s) { return s ? s->h_actions : nullptr; }
-void *cog_sampler_device_actions(cog_sampler *s) { return s ? (void *)s->d_actions : nullptr; }
+void *cog_sampler_device_actions(cog_sampler *s) { return s ? (void *)s->sh[0].d_actions : nullptr; }
+void *cog_sampler_shard_device_actions(cog_sampler *s, int k) {
+  if (!s || k < 0 || (size_t)k >= s->sh.size()) return nullptr;
+  return (void *)s->sh[k].d_actions;
+}
+int cog_sampler_device(const cog_sampler *s) { return s ? s->sh[0].device : -1; }
 
 // ---- runner ------------------------------------------------------------------------------
 int cog_runner_create(cog_env *env, cog_sampler *s, size_t n_threads, uint32_t flags, cog_runner **out) {
   if (!env || !s || !out) return fail(COG_ERR_INVALID, "NULL argument");
-  if (env->s.n != s->n) return fail(COG_ERR_INVALID, "env and sampler batch sizes differ");
-  if (env->device != s->device) return fail(COG_ERR_INVALID, "env and sampler are on different devices");
+  if (env->n != s->n) return fail(COG_ERR_INVALID, "env and sampler batch sizes differ");
+  if (env->sh.size() != s->sh.size()) return fail(COG_ERR_INVALID, "env and sampler are sharded differently");
+  for (size_t j = 0; j < env->sh.size(); j++)
+    if (env->sh[j].device != s->sh[j].device || env->sh[j].first != s->sh[j].first || env->sh[j].n != s->sh[j].n)
+      return fail(COG_ERR_INVALID, "env and sampler are on different devices");
   cog_runner *r = new cog_runner();
   r->env = env;
   r->smp = s;
   r->n_threads = n_threads;
   r->flags = flags;
+  r->ev.resize(env->sh.size());
   const char *cv = std::getenv("COG_RUNNER_CHUNK");        // default rollout steps per launch
   r->chunk = cv ? std::max(1, std::atoi(cv)) : 1;
   *out = r;
@@ -504,53 +836,72 @@ int cog_runner_create(cog_env *env, cog_sampler *s, size_t n_threads, uint32_t f
 
 void cog_runner_destroy(cog_runner *r) {
   if (!r) return;
-  DeviceGuard g(r->env->device);
-  (void)hipStreamSynchronize(r->env->stream);
-  for (hipEvent_t ev : r->ev) (void)hipEventDestroy(ev);
+  for (size_t j = 0; j < r->env->sh.size(); j++) {
+    DeviceGuard g(r->env->sh[j].device);
+    (void)hipStreamSynchronize(r->env->sh[j].stream);
+    for (hipEvent_t ev : r->ev[j]) (void)hipEventDestroy(ev);
+  }
   delete r;
 }
 
 size_t cog_runner_n_threads(const cog_runner *r) { return r ? r->n_threads : 0; }
+
+static bool runner_host(const cog_runner *r) { return !(r->flags & COG_RUNNER_DEVICE_VIEWS) && r->env->host; }
 
 static int runner_flush_sample(cog_runner *r) {
   if (!r->pending_sample) return COG_OK;
   r->pending_sample = false;
   // a lone sample reads the selected masks, as the reference runner's does (runner.h:26,48);
   // stored-mask sampling exists only fused with a step
-  return sampler_run(r->smp, r->env->s.sel, r->env->stream, false);
-}
-
-static int runner_timing_event(cog_runner *r, hipEvent_t *out) {
-  if (r->ev_used + 1 > r->ev.size()) {
-    hipEvent_t ev;
-    HIPCHK(hipEventCreate(&ev));
-    r->ev.push_back(ev);
+  for (size_t j = 0; j < r->env->sh.size(); j++) {
+    EnvShard &k = r->env->sh[j];
+    DeviceGuard g(k.device);
+    int rc = sampler_run(r->smp->sh[j], r->smp->h_actions, k.s.sel, k.stream, false);
+    if (rc) return rc;
   }
-  *out = r->ev[r->ev_used++];
-  HIPCHK(hipEventRecord(*out, r->env->stream));
   return COG_OK;
 }
 
-// `steps` back-to-back fused sample+step launches; with timing on, one event pair brackets the
-// batch (device time per launch = pair time / steps, the same quantity rocprofv3's kernel
-// trace averages, without per-launch event overhead)
+static int runner_timing_event(cog_runner *r, size_t j) {
+  std::vector<hipEvent_t> &v = r->ev[j];
+  while (r->ev_used + 1 >= v.size()) {
+    hipEvent_t ev;
+    HIPCHK(hipEventCreate(&ev));
+    v.push_back(ev);
+  }
+  return COG_OK;
+}
+
+// `steps` fused sample+step launches on every shard; with timing on, one event pair per shard
+// brackets the batch (device time per launch = pair time / steps, the quantity rocprofv3's
+// kernel trace averages, without per-launch event overhead)
 static int runner_launch_fused(cog_runner *r, int steps) {
-  hipEvent_t ev;
-  int rc;
-  if (r->timing && (rc = runner_timing_event(r, &ev))) return rc;
   const int src = (r->flags & COG_RUNNER_STORED_MASKS) ? cog::MASK_STORED : cog::MASK_SELECTED;
-  if (r->chunk > 1) {                                      // persistent kernels, chunk steps each
-    for (int t = 0; t < steps; t += r->chunk)
-      if (cog::launch_rollout(r->env->s, src, std::min(r->chunk, steps - t), r->smp->d_rng, r->smp->d_actions,
-                              r->env->stream))
-        return fail(COG_ERR_HIP, std::string("rollout launch failed: ") + hipGetErrorString(hipGetLastError()));
-  } else {
-    for (int t = 0; t < steps; t++)
-      if (cog::launch_sample_step(r->env->s, src, r->smp->d_rng, r->smp->d_actions, r->env->stream))
-        return fail(COG_ERR_HIP, std::string("sample_step launch failed: ") + hipGetErrorString(hipGetLastError()));
+  const bool host = runner_host(r);
+  int rc;
+  if (host && (rc = prepare_host(r->env))) return rc;
+  for (size_t j = 0; j < r->env->sh.size(); j++) {
+    EnvShard &k = r->env->sh[j];
+    SamplerShard &q = r->smp->sh[j];
+    DeviceGuard g(k.device);
+    if (r->timing) {
+      if ((rc = runner_timing_event(r, j))) return rc;
+      HIPCHK(hipEventRecord(r->ev[j][r->ev_used], k.stream));
+    }
+    const cog::DevState s = launch_state(k, host);
+    if (r->chunk > 1) {                                    // persistent kernels, chunk steps each
+      for (int t = 0; t < steps; t += r->chunk)
+        if (cog::launch_rollout(s, src, std::min(r->chunk, steps - t), q.d_rng, q.d_actions, k.stream))
+          return fail(COG_ERR_HIP, std::string("rollout launch failed: ") + hipGetErrorString(hipGetLastError()));
+    } else {
+      for (int t = 0; t < steps; t++)
+        if (cog::launch_sample_step(s, src, q.d_rng, q.d_actions, k.stream))
+          return fail(COG_ERR_HIP, std::string("sample_step launch failed: ") + hipGetErrorString(hipGetLastError()));
+    }
+    if (r->timing) HIPCHK(hipEventRecord(r->ev[j][r->ev_used + 1], k.stream));
   }
   if (r->timing) {
-    if ((rc = runner_timing_event(r, &ev))) return rc;
+    r->ev_used += 2;
     r->timed_launches += (uint64_t)steps;
   }
   return COG_OK;
@@ -558,7 +909,6 @@ static int runner_launch_fused(cog_runner *r, int steps) {
 
 int cog_runner_sample(cog_runner *r) {
   if (!r) return fail(COG_ERR_INVALID, "runner is NULL");
-  DeviceGuard g(r->env->device);
   int rc = runner_flush_sample(r);   // two samples in a row: the first one still runs
   if (rc) return rc;
   r->pending_sample = true;
@@ -567,19 +917,24 @@ int cog_runner_sample(cog_runner *r) {
 
 int cog_runner_step(cog_runner *r) {
   if (!r) return fail(COG_ERR_INVALID, "runner is NULL");
-  DeviceGuard g(r->env->device);
   if (r->pending_sample) {
     r->pending_sample = false;
     return runner_launch_fused(r, 1);
   }
-  if (cog::launch_step(r->env->s, r->smp->d_actions, r->env->stream))
-    return fail(COG_ERR_HIP, std::string("step launch failed: ") + hipGetErrorString(hipGetLastError()));
+  const bool host = runner_host(r);
+  int rc;
+  if (host && (rc = prepare_host(r->env))) return rc;
+  for (size_t j = 0; j < r->env->sh.size(); j++) {
+    EnvShard &k = r->env->sh[j];
+    DeviceGuard g(k.device);
+    if (cog::launch_step(launch_state(k, host), r->smp->sh[j].d_actions, k.stream))
+      return fail(COG_ERR_HIP, std::string("step launch failed: ") + hipGetErrorString(hipGetLastError()));
+  }
   return COG_OK;
 }
 
 int cog_runner_rollout(cog_runner *r, int steps) {
   if (!r || steps < 0) return fail(COG_ERR_INVALID, "bad argument");
-  DeviceGuard g(r->env->device);
   int rc = runner_flush_sample(r);
   if (rc) return rc;
   return steps ? runner_launch_fused(r, steps) : COG_OK;
@@ -587,14 +942,20 @@ int cog_runner_rollout(cog_runner *r, int steps) {
 
 int cog_runner_sync(cog_runner *r) {
   if (!r) return fail(COG_ERR_INVALID, "runner is NULL");
-  DeviceGuard g(r->env->device);
   int rc = runner_flush_sample(r);
   if (rc) return rc;
   const bool host = !(r->flags & COG_RUNNER_DEVICE_VIEWS);
-  if (host && r->smp->n)
-    HIPCHK(hipMemcpyAsync(r->smp->h_actions, r->smp->d_actions, r->smp->n * COG_ACTION_BYTES,
-                          hipMemcpyDeviceToHost, r->env->stream));
-  return finish_steps(r->env, host);
+  if (host) {
+    for (size_t j = 0; j < r->env->sh.size(); j++) {
+      EnvShard &k = r->env->sh[j];
+      SamplerShard &q = r->smp->sh[j];
+      if (!q.n) continue;
+      DeviceGuard g(k.device);
+      HIPCHK(hipMemcpyAsync(r->smp->h_actions + q.first, q.d_actions, q.n * COG_ACTION_BYTES, hipMemcpyDeviceToHost,
+                            k.stream));
+    }
+  }
+  return finish(r->env, host);
 }
 
 int cog_runner_set_chunk(cog_runner *r, int steps_per_launch) {
@@ -611,17 +972,22 @@ int cog_runner_set_timing(cog_runner *r, int enable) {
   return COG_OK;
 }
 
+// device time: per shard the sum over its event pairs; the slowest shard's total
 int cog_runner_kernel_time(cog_runner *r, double *total_ms, uint64_t *launches) {
   if (!r) return fail(COG_ERR_INVALID, "runner is NULL");
-  DeviceGuard g(r->env->device);
-  HIPCHK(hipStreamSynchronize(r->env->stream));
-  double acc = 0.0;
-  for (size_t k = 0; k + 1 < r->ev_used; k += 2) {
-    float ms = 0.f;
-    HIPCHK(hipEventElapsedTime(&ms, r->ev[k], r->ev[k + 1]));
-    acc += ms;
+  int rc = sync_all(r->env);
+  if (rc) return rc;
+  double worst = 0.0;
+  for (size_t j = 0; j < r->env->sh.size(); j++) {
+    double acc = 0.0;
+    for (size_t q = 0; q + 1 < r->ev_used && q + 1 < r->ev[j].size(); q += 2) {
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, r->ev[j][q], r->ev[j][q + 1]));
+      acc += ms;
+    }
+    worst = std::max(worst, acc);
   }
-  if (total_ms) *total_ms = acc;
+  if (total_ms) *total_ms = worst;
   if (launches) *launches = r->timed_launches;
   r->ev_used = 0;
   r->timed_launches = 0;

@@ -95,10 +95,11 @@ struct DevState {
   uint4 *heads;                      // [n][5] mask bit-vectors: selected, stored of players 0..3
   GenScratch *gen;
   uint32_t *status;                  // [0] OR of error flags, [1] error count, [2] dirty count
-  uint32_t *dirty;                   // [cap] envs whose map was re-generated (host view refresh)
-  uint32_t *park;                    // [n] rollout hand-over: step of a pending episode end, or ~0
-  size_t first;                      // global index of env 0 (sub-range launches; dirty list ids)
-  size_t cap;                        // capacity of the dirty list
+  uint32_t *dirty;                   // [cap] local indices of envs whose map was re-generated
+  uint32_t *err;                     // host-mapped word (pinned): set to 1 on any error, so a sync
+                                     // learns "no error" without a device-to-host copy
+  size_t first;                      // global index of env 0 of this shard (seeds are seed + global index)
+  size_t cap;                        // capacity of the dirty list; 0: no list (outputs stay on the device)
   uint32_t autoreset;                // 1: vec_cog_env (reset a finished env in the same call,
                                      // vec_environment.h:56-59); 0: cog_env (stays done)
   unsigned long long *stamps;        // diagnostic builds (COG_STAMPS) only: per-wave phase clocks
@@ -109,26 +110,6 @@ struct ResetParams {
   uint8_t n_players, n_pieces, difficulty, use_params;   // use_params=0: cog_env::reset()
   uint32_t max_steps;
 };
-
-// the envs [lo, hi) of s as a state of their own (per-stream sub-range launches)
-inline DevState sub_state(const DevState &s, size_t lo, size_t hi) {
-  DevState t = s;
-  t.n = hi - lo;
-  t.first = s.first + lo;
-  t.obs += lo * COG_OBS_BYTES;
-  t.sel += lo * COG_MASK_BYTES;
-  t.info += lo * COG_INFO_BYTES;
-  t.rew += lo * 4;
-  t.done += lo;
-  t.agent += lo;
-  t.priv += lo;
-  t.grid += lo * (size_t)kGridBytes;
-  t.cgrid += lo * (size_t)COG_CELLS;
-  t.heads += lo * 5;
-  t.park += lo;
-  t.gen += lo;
-  return t;
-}
 
 enum MaskSource : int { MASK_SELECTED = 0, MASK_STORED = 1, MASK_EXTERNAL = 2 };
 
@@ -144,6 +125,6 @@ int launch_sample_step(const DevState &s, int mask_source, uint32_t *d_rng, uint
                        void *stream);
 int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions,
                    void *stream);                    // persistent K-step runner loop
-int launch_seed_sampler(size_t n, uint32_t seed, uint32_t *d_rng, void *stream);
+int launch_seed_sampler(size_t n, uint64_t seed, size_t first, uint32_t *d_rng, void *stream);
 
 }  // namespace cog

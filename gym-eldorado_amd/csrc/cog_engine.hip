@@ -671,13 +671,14 @@ DEV void build_cgrid(const Ctx &e) {
 DEV void wave_encode(const DevState &s, size_t i, bool enc) {
   uint64_t m = __ballot(enc);
   const int lane = threadIdx.x & 63;
+  const int nl = blockDim.x < 64 ? (int)blockDim.x : 64;  // active lanes (narrow workgroups)
   while (m) {
     const int l = __ffsll((unsigned long long)m) - 1;
     m &= m - 1;
     const size_t env = (size_t)__shfl((int)i, l);
     const uint8_t *cg = s.cgrid + env * COG_CELLS;
     uint8_t *map = s.obs + env * COG_OBS_BYTES;
-    for (int k = lane; k < kEncBlocks; k += 64) encode_block(cg, map, k);
+    for (int k = lane; k < kEncBlocks; k += nl) encode_block(cg, map, k);
   }
 }
 
@@ -690,7 +691,7 @@ __global__ void k_init(DevState s, uint32_t default_seed) {
   EnvPriv *pv = s.priv + i;
   EnvPriv z;
   memset(&z, 0, sizeof(z));
-  z.seed = default_seed + (uint32_t)i;
+  z.seed = default_seed + (uint32_t)(s.first + i);
   z.rng = mr_seed(z.seed);
   z.n_players = 4; z.n_pieces = 3; z.difficulty = 0; z.max_steps = 100000;
   z.n_in_market = COG_MKT_SLOTS;
@@ -720,12 +721,13 @@ __global__ void k_reset(DevState s, ResetParams p) {
     pv->n_pieces = p.n_pieces;
     pv->difficulty = p.difficulty;
     pv->max_steps = p.max_steps;
-    pv->seed = p.seed + (uint32_t)i;                       // vec_environment.h:41, u32 wrap (Q33)
+    pv->seed = p.seed + (uint32_t)(s.first + i);           // vec_environment.h:41, u32 wrap (Q33)
     pv->rng = mr_seed(pv->seed);
   }
   if (!env_reset(e)) {
     atomicOr(&s.status[0], pv->flags);
     atomicAdd(&s.status[1], 1u);
+    *s.err = 1u;                                           // host-visible error flag
   }
 }
 
@@ -1829,10 +1831,13 @@ DEV bool end_of_step(const DevState &s, size_t i, bool was_done, bool finish, ui
     if (!env_reset(e)) {
       atomicOr(&s.status[0], e.pv->flags);
       atomicAdd(&s.status[1], 1u);
+      *s.err = 1u;                                         // host-visible error flag
     } else {
       enc = true;
-      const uint32_t k = atomicAdd(&s.status[2], 1u);
-      if (k < s.cap) s.dirty[k] = (uint32_t)(s.first + i);
+      if (s.cap) {                                         // host views: list the regenerated maps
+        const uint32_t k = atomicAdd(&s.status[2], 1u);
+        if (k < s.cap) s.dirty[k] = (uint32_t)i;
+      }
     }
     sync_heads(s, i);
     agent = e.pv->agent;
@@ -1892,12 +1897,14 @@ __global__ void __launch_bounds__(64) k_env_step(DevState s, const uint8_t *__re
 // step is the reference's); what changes is where the next step reads its inputs from: the
 // env-level records stay in VGPRs and every player's records (deck, counters, neighbourhood
 // cache, stored mask) in this wave's LDS, so a step issues no global loads unless it resets.
+template <int NL>                     // NL: envs (lanes) per workgroup
 struct LaneLds {
-  uint4 deck[4][7][64];               // [player][granule][lane]: lane-contiguous, conflict-free
-  uint4 pl[4][64];
-  uint2 cells[4][64];
-  uint4 heads[4][64];                 // stored masks (MBits + pad)
+  uint4 deck[4][7][NL];               // [player][granule][lane]: lane-contiguous, conflict-free
+  uint4 pl[4][NL];
+  uint2 cells[4][NL];
+  uint4 heads[4][NL];                 // stored masks (MBits + pad)
 };
+template <class LaneLds>
 DEV void lds_fill_players(LaneLds &L, const DevState &s, size_t i, int l) {
   const uint4 *pv4 = reinterpret_cast<const uint4 *>(s.priv + i);
 #pragma unroll
@@ -1912,6 +1919,7 @@ DEV void lds_fill_players(LaneLds &L, const DevState &s, size_t i, int l) {
 }
 // every private record of env i (EnvPriv granules 0, 1, 3, all players, all mask bit vectors)
 // from the rollout's on-chip copies
+template <class LaneLds>
 DEV void store_private_all(const DevState &s, size_t i, const Snap &S, const LaneLds &L, int l) {
   uint4 *pw = reinterpret_cast<uint4 *>(s.priv + i);
   pw[0] = S.g0;
@@ -1925,6 +1933,7 @@ DEV void store_private_all(const DevState &s, size_t i, const Snap &S, const Lan
     s.heads[5 * i + 1 + p] = L.heads[p][l];
   }
 }
+template <class LaneLds>
 DEV void lds_players(const LaneLds &L, int l, int ag, int na, Snap &S) {
   S.pla = L.pl[ag][l];
   S.pln = L.pl[na][l];
@@ -1936,28 +1945,25 @@ DEV void lds_players(const LaneLds &L, int l, int ag, int na, Snap &S) {
   for (int k = 0; k < 7; k++) S.dk[k] = L.deck[ag][k][l];
 }
 
-// The rollout is two kernels.  k_env_rollout<SRC, false> ("lean") carries no episode-end code:
-// a lane whose env finishes (or starts done) at step t stores its state, records t in park[i]
-// and leaves the loop; the other lanes go on.  k_env_rollout<SRC, true> ("fix-up"), launched
-// right after it on the same stream, picks up exactly those envs: it completes step t's episode
-// end (finish_episode, dones, auto-reset, encode) and runs the env's remaining steps with the
-// full step (resets included).  Nothing reads the envs between the two launches, and envs are
-// independent (no barrier between the reference's workers either, runner.h:39-62), so the
-// outputs are the single-kernel ones; the lean kernel's loop drops the reset path's registers
-// (no AGPR or scratch spills: 214 VGPRs).  Lanes with nothing parked leave the fix-up at once.
+// The rollout is one kernel in two passes.  The lean pass (FIX = false) carries no episode-end
+// code: a lane whose env finishes (or starts done) at step t stores its state, keeps t (its
+// "park" code) and leaves the loop; the other lanes go on.  After the loop, a wave with a parked
+// lane runs the fix-up pass (FIX = true, a wave-uniform branch) for exactly those lanes: it
+// completes step t's episode end (finish_episode, dones, auto-reset, encode) and runs the env's
+// remaining steps with the full step (resets included).  Nothing reads the env in between and
+// envs are independent (no barrier between the reference's workers either, runner.h:39-62), so
+// the outputs are those of one full-step loop; the lean loop keeps the reset path's registers
+// out of its allocation.  A wave with nothing parked ends after the lean pass (round 1 launched
+// the fix-up as a second kernel: 4.8 us per launch even when it had nothing to do).
 constexpr uint32_t kParkNone = ~0u, kParkFinish = 1u << 31;
-template <int SRC, bool FIX>
-__global__ void __launch_bounds__(64) k_env_rollout(DevState s, int steps, uint32_t *__restrict__ rngs,
-                                                    uint8_t *__restrict__ actions_out) {
-  __shared__ LaneLds L;
+template <int SRC, bool FIX, int NL>
+DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s, int steps, uint32_t *__restrict__ rngs,
+                          uint8_t *__restrict__ actions_out, uint32_t park) {
   const int l = threadIdx.x;
   const size_t i0 = (size_t)blockIdx.x * blockDim.x + l;
   const size_t i = i0 < s.n ? i0 : 0;
   int t_first = 0;                                         // fix-up: this lane's first full step
-  uint32_t park = kParkNone;
-  if (FIX && i0 < s.n) park = s.park[i];
   bool live = i0 < s.n && (!FIX || park != kParkNone);
-  if (FIX && !__builtin_amdgcn_ballot_w64(live)) return;  // (wave-uniform exit)
   Snap S;
   uint32_t srng = 0, out = ~0u;                           // out: end_of_step's output cache
   auto next_of = [&](int a) { return a + 1 >= (int)(S.g1.x & 0xffu) ? 0 : a + 1; };   // n_players
@@ -1969,7 +1975,6 @@ __global__ void __launch_bounds__(64) k_env_rollout(DevState s, int steps, uint3
   if (FIX) {                                               // step `park`'s episode end
     bool enc = false;
     if (live) {
-      s.park[i] = kParkNone;
       t_first = (int)(park & ~kParkFinish) + 1;
       uint32_t agent = S.g1.y & 0xffu;
       const bool finish = (park & kParkFinish) != 0u;
@@ -2034,9 +2039,9 @@ __global__ void __launch_bounds__(64) k_env_rollout(DevState s, int steps, uint3
       uint32_t agent = R.agent();
       if (was_done || finish) {                            // episode end: state to HBM first
         store_private_all(s, i, S, L, l);
-        if (!FIX) {                                        // hand the env to the fix-up kernel
+        if (!FIX) {                                        // hand the env to the fix-up pass
           rngs[i] = srng;
-          s.park[i] = (uint32_t)t | (finish ? kParkFinish : 0u);
+          park = (uint32_t)t | (finish ? kParkFinish : 0u);
           live = false;
           continue;
         }
@@ -2058,8 +2063,19 @@ __global__ void __launch_bounds__(64) k_env_rollout(DevState s, int steps, uint3
     store_private_all(s, i, S, L, l);
     rngs[i] = srng;
   }
-  PH_FLUSH(s);
+  if (!FIX) PH_FLUSH(s);
+  return FIX ? kParkNone : park;
 }
+
+template <int SRC, int NL>
+__global__ void __launch_bounds__(NL) k_env_rollout(DevState s, int steps, uint32_t *__restrict__ rngs,
+                                                    uint8_t *__restrict__ actions_out) {
+  __shared__ LaneLds<NL> L;
+  const uint32_t park = rollout_pass<SRC, false, NL>(L, s, steps, rngs, actions_out, kParkNone);
+  if (__builtin_amdgcn_ballot_w64(park != kParkNone))    // (wave-uniform)
+    rollout_pass<SRC, true, NL>(L, s, steps, rngs, actions_out, park);
+}
+
 
 __global__ void __launch_bounds__(256) k_sample(size_t n, const uint8_t *__restrict__ masks,
                                                 uint32_t *__restrict__ rngs, uint8_t *__restrict__ actions) {
@@ -2077,9 +2093,9 @@ __global__ void k_sync_heads(DevState s) {
   if (i < s.n) sync_heads(s, i);
 }
 
-__global__ void k_seed_sampler(size_t n, uint32_t seed, uint32_t *rngs) {
+__global__ void k_seed_sampler(size_t n, uint64_t seed, size_t first, uint32_t *rngs) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) rngs[i] = mr_seed((uint64_t)seed + (uint64_t)i);   // vec_sampler.h:9-13 (no u32 wrap)
+  if (i < n) rngs[i] = mr_seed(seed + (uint64_t)(first + i));   // vec_sampler.h:9-13 (no u32 wrap)
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2131,22 +2147,27 @@ int launch_sample_step(const DevState &s, int mask_source, uint32_t *d_rng, uint
                        nullptr, d_rng, d_actions);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+template <int NL>
+static void rollout_launch(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions,
+                           hipStream_t st) {
+  const dim3 g(blocks_for(s.n, NL)), b(NL);
+  if (mask_source == MASK_STORED)
+    hipLaunchKernelGGL((k_env_rollout<MASK_STORED, NL>), g, b, 0, st, s, steps, d_rng, d_actions);
+  else
+    hipLaunchKernelGGL((k_env_rollout<MASK_SELECTED, NL>), g, b, 0, st, s, steps, d_rng, d_actions);
+}
 int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions, void *stream) {
   if (!s.n || steps <= 0) return 0;
-  const dim3 g(blocks_for(s.n, 64)), b(64);
-  const hipStream_t st = (hipStream_t)stream;
-  if (mask_source == MASK_STORED) {
-    hipLaunchKernelGGL((k_env_rollout<MASK_STORED, false>), g, b, 0, st, s, steps, d_rng, d_actions);
-    hipLaunchKernelGGL((k_env_rollout<MASK_STORED, true>), g, b, 0, st, s, steps, d_rng, d_actions);
-  } else {
-    hipLaunchKernelGGL((k_env_rollout<MASK_SELECTED, false>), g, b, 0, st, s, steps, d_rng, d_actions);
-    hipLaunchKernelGGL((k_env_rollout<MASK_SELECTED, true>), g, b, 0, st, s, steps, d_rng, d_actions);
-  }
+  // one 64-env wave per workgroup: 32-env workgroups (two waves per SIMD at 65,536 envs) measured
+  // 7.3 us/step against 3.8 (tools/lanes_ab.sh, round 2): the SIMD already issues one of this
+  // integer code's instructions per quad-cycle with a single wave
+  rollout_launch<64>(s, mask_source, steps, d_rng, d_actions, (hipStream_t)stream);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-int launch_seed_sampler(size_t n, uint32_t seed, uint32_t *d_rng, void *stream) {
+int launch_seed_sampler(size_t n, uint64_t seed, size_t first, uint32_t *d_rng, void *stream) {
   if (!n) return 0;
-  hipLaunchKernelGGL(k_seed_sampler, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, n, seed, d_rng);
+  hipLaunchKernelGGL(k_seed_sampler, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, n, seed, first,
+                     d_rng);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

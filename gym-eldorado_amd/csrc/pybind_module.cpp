@@ -17,6 +17,8 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <vector>
+#include <algorithm>
 
 #include "../../include/cog.h"
 
@@ -78,12 +80,46 @@ static void check(int rc) {
   throw std::runtime_error(msg);
 }
 
-static int default_device() {
-  const char *d = std::getenv("COG_DEVICE");
-  if (d && *d) return std::atoi(d);
+// Devices of a new handle (reference: one object owns every env, vectorized.h:185-214).
+//   device=None: COG_DEVICES ("0,2,..."), else LOCAL_RANK (one process per GPU under torchrun),
+//                else COG_DEVICE, else every visible GPU with at least kMinShard envs per shard
+//                (a small batch stays on one GPU);
+//   device=int:  that GPU;  device=[d0, d1, ...]: one contiguous shard per entry.
+constexpr size_t kMinShard = 8192;
+static std::vector<int> parse_list(const char *v) {
+  std::vector<int> out;
+  const char *p = v;
+  while (*p) {
+    char *end = nullptr;
+    const long d = std::strtol(p, &end, 10);
+    if (end == p) throw py::value_error(std::string("bad device list: ") + v);
+    out.push_back((int)d);
+    p = *end == ',' ? end + 1 : end;
+    if (*end && *end != ',') throw py::value_error(std::string("bad device list: ") + v);
+  }
+  if (out.empty()) throw py::value_error("empty device list");
+  return out;
+}
+static std::vector<int> default_devices(size_t n) {
+  const char *v = std::getenv("COG_DEVICES");
+  if (v && *v) return parse_list(v);
   const char *lr = std::getenv("LOCAL_RANK");
-  if (lr && *lr) return std::atoi(lr);
-  return 0;
+  if (lr && *lr) return {std::atoi(lr)};
+  const char *d = std::getenv("COG_DEVICE");
+  if (d && *d) return {std::atoi(d)};
+  int cnt = 0;
+  if (cog_device_count(&cnt) != COG_OK || cnt <= 1) return {0};
+  const size_t k = std::min<size_t>((size_t)cnt, std::max<size_t>(1, n / kMinShard));
+  std::vector<int> out;
+  for (size_t j = 0; j < k; j++) out.push_back((int)j);
+  return out;
+}
+static std::vector<int> devices_of(const py::object &device, size_t n) {
+  if (device.is_none()) return default_devices(n);
+  if (py::isinstance<py::int_>(device)) return {device.cast<int>()};
+  std::vector<int> out = device.cast<std::vector<int>>();
+  if (out.empty()) throw py::value_error("device list is empty");
+  return out;
 }
 
 template <class T>
@@ -170,7 +206,10 @@ static py::capsule dl_capsule(void *p, int device, size_t n, int64_t width, uint
 // ---- vec env (py_vec_env, vectorized.h:25-105) -------------------------------------------
 class VecEnv {
  public:
-  VecEnv(size_t n, std::optional<int> device) : n_(n) { check(cog_env_create(n, device.value_or(default_device()), &h_)); }
+  VecEnv(size_t n, const py::object &device) : n_(n) {
+    const std::vector<int> d = devices_of(device, n);
+    check(cog_env_create_multi(n, d.data(), (int)d.size(), &h_));
+  }
   ~VecEnv() { cog_env_destroy(h_); }
   VecEnv(const VecEnv &) = delete;
   VecEnv &operator=(const VecEnv &) = delete;
@@ -188,6 +227,16 @@ class VecEnv {
     check(cog_env_get_views(h_, &v));
     return v;
   }
+  cog_env_views shard_views(int k) {
+    cog_env_views v;
+    check(cog_env_shard_views(h_, k, &v));
+    return v;
+  }
+  int num_shards() const {
+    int k = 0;
+    check(cog_env_num_shards(h_, &k));
+    return k;
+  }
   size_t num_envs() const { return n_; }
   cog_env *handle() { return h_; }
 
@@ -199,9 +248,10 @@ class VecEnv {
 // ---- vec sampler (py_vec_action_sampler, vectorized.h:107-127) ----------------------------
 class VecSampler {
  public:
-  VecSampler(size_t n, std::optional<size_t> seed, std::optional<int> device) : n_(n) {
+  VecSampler(size_t n, std::optional<size_t> seed, const py::object &device) : n_(n) {
     const uint32_t s = (uint32_t)seed.value_or(std::random_device{}());   // u32 as in vectorized.h:113
-    check(cog_sampler_create(n, s, device.value_or(default_device()), &h_));
+    const std::vector<int> d = devices_of(device, n);
+    check(cog_sampler_create_multi(n, s, d.data(), (int)d.size(), &h_));
   }
   ~VecSampler() { cog_sampler_destroy(h_); }
   VecSampler(const VecSampler &) = delete;
@@ -287,7 +337,7 @@ PYBIND11_MODULE(_city_of_gold, m) {
   });
 
   py::class_<VecEnv>(m, "VecEnvBase", py::dynamic_attr())
-      .def(py::init<size_t, std::optional<int>>(), "n_envs"_a, "device"_a = py::none())
+      .def(py::init<size_t, const py::object &>(), "n_envs"_a, "device"_a = py::none())
       .def("reset", &VecEnv::reset_default, "Reset all environments, keeping parameters (vectorized.h:187-195)")
       .def("reset", &VecEnv::reset, "seed"_a, "n_players"_a, "n_pieces"_a, "difficulty"_a, "max_steps"_a, "render"_a)
       .def("step", &VecEnv::step, "actions"_a)
@@ -322,18 +372,27 @@ PYBIND11_MODULE(_city_of_gold, m) {
         auto v = e.views();
         return view(reinterpret_cast<Info *>(v.infos), v.n_envs, self);
       })
-      .def("device_pointers", [](VecEnv &e) {
-        auto v = e.views();
+      .def_property_readonly("num_shards", &VecEnv::num_shards)
+      .def("shard_info", [](VecEnv &e, int k) {
+        size_t first = 0, count = 0;
+        int dev = 0;
+        check(cog_env_shard_info(e.handle(), k, &first, &count, &dev));
+        return py::make_tuple(first, count, dev);
+      }, "shard"_a)
+      .def("device_pointers", [](VecEnv &e, int k) {
+        auto v = e.shard_views(k);
         return py::dict("observations"_a = (uintptr_t)v.d_observations,
                         "selected_action_masks"_a = (uintptr_t)v.d_selected_action_masks,
                         "rewards"_a = (uintptr_t)v.d_rewards, "dones"_a = (uintptr_t)v.d_dones,
                         "agent_selection"_a = (uintptr_t)v.d_agent_selection, "infos"_a = (uintptr_t)v.d_infos);
-      })
-      .def("dlpack", [](py::object self, const std::string &name) {
-        // one device view as a DLPack capsule (torch.from_dlpack, TensorDict); rows are records
+      }, "shard"_a = 0)
+      .def("dlpack", [](py::object self, const std::string &name, int k) {
+        // one device view of shard k as a DLPack capsule (torch.from_dlpack, TensorDict); rows are records
         VecEnv &e = self.cast<VecEnv &>();
-        auto v = e.views();
-        const int dev = cog_env_device(e.handle());
+        auto v = e.shard_views(k);
+        size_t first = 0, count = 0;
+        int dev = 0;
+        check(cog_env_shard_info(e.handle(), k, &first, &count, &dev));
         const size_t n = v.n_envs;
         if (name == "observations") return dl_capsule(v.d_observations, dev, n, sizeof(ObsData), kDLUInt, 8, self);
         if (name == "selected_action_masks")
@@ -343,13 +402,21 @@ PYBIND11_MODULE(_city_of_gold, m) {
         if (name == "agent_selection") return dl_capsule(v.d_agent_selection, dev, n, 0, kDLUInt, 8, self);
         if (name == "infos") return dl_capsule(v.d_infos, dev, n, sizeof(Info), kDLUInt, 8, self);
         throw py::value_error("no device view named " + name);
-      }, "name"_a)
-      .def("step_device", [](VecEnv &e, uintptr_t d_actions) {
-        // step with ActionData records already in device memory (e.g. a torch tensor's data_ptr())
-        check(cog_env_step_device(e.handle(), reinterpret_cast<const void *>(d_actions), e.num_envs()));
-      }, "d_actions"_a)
+      }, "name"_a, "shard"_a = 0)
+      .def("step_device", [](VecEnv &e, uintptr_t d_actions, uintptr_t stream) {
+        // step with ActionData records already in device memory (e.g. a torch tensor's data_ptr()),
+        // ordered after the work queued on `stream` (0: none)
+        check(cog_env_step_device_stream(e.handle(), reinterpret_cast<const void *>(d_actions), e.num_envs(),
+                                         reinterpret_cast<void *>(stream)));
+      }, "d_actions"_a, "stream"_a = 0)
+      .def("wait_stream", [](VecEnv &e, uintptr_t stream, int k) {
+        check(cog_env_wait_stream(e.handle(), k, reinterpret_cast<void *>(stream)));
+      }, "stream"_a, "shard"_a = 0)
+      .def("signal_stream", [](VecEnv &e, uintptr_t stream, int k) {
+        check(cog_env_signal_stream(e.handle(), k, reinterpret_cast<void *>(stream)));
+      }, "stream"_a, "shard"_a = 0)
       .def("set_autoreset", [](VecEnv &e, bool on) { check(cog_env_set_autoreset(e.handle(), on ? 1 : 0)); }, "on"_a)
-      .def("stream", [](VecEnv &e) { return (uintptr_t)cog_env_stream(e.handle()); })
+      .def("stream", [](VecEnv &e, int k) { return (uintptr_t)cog_env_shard_stream(e.handle(), k); }, "shard"_a = 0)
       .def("hazards", [](VecEnv &e) {
         py::array_t<uint32_t> per((py::ssize_t)e.num_envs());
         uint32_t acc = 0;
@@ -365,16 +432,26 @@ PYBIND11_MODULE(_city_of_gold, m) {
       }, "iters"_a = 20, "variant"_a = 0);
 
   py::class_<VecSampler>(m, "VecSamplerBase", py::dynamic_attr())
-      .def(py::init<size_t, std::optional<size_t>, std::optional<int>>(), "n_envs"_a, "seed"_a = py::none(),
+      .def(py::init<size_t, std::optional<size_t>, const py::object &>(), "n_envs"_a, "seed"_a = py::none(),
            "device"_a = py::none())
       .def("get_actions", [](py::object self) {
         VecSampler &s = self.cast<VecSampler &>();
         return view(s.actions(), s.num_envs(), self);
       })
       .def("sample", &VecSampler::sample, "action_mask"_a)
-      .def("device_actions", [](VecSampler &s) { return (uintptr_t)cog_sampler_device_actions(s.handle()); })
-      .def("dlpack", [](py::object self) {       // the device actions (ActionData rows)
+      .def("device_actions", [](VecSampler &s, int k) {
+        return (uintptr_t)cog_sampler_shard_device_actions(s.handle(), k);
+      }, "shard"_a = 0)
+      .def_property_readonly("num_shards", [](VecSampler &s) {
+        int k = 0;
+        check(cog_sampler_num_shards(s.handle(), &k));
+        return k;
+      })
+      .def("dlpack", [](py::object self) {       // the device actions (ActionData rows), single shard
         VecSampler &s = self.cast<VecSampler &>();
+        int k = 0;
+        check(cog_sampler_num_shards(s.handle(), &k));
+        if (k != 1) throw py::value_error("dlpack() of a multi-shard sampler: use device_actions(shard)");
         return dl_capsule(cog_sampler_device_actions(s.handle()), cog_sampler_device(s.handle()), s.num_envs(),
                           sizeof(ActionData), kDLUInt, 8, self);
       });

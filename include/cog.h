@@ -99,6 +99,14 @@ COG_API int cog_device_count(int *out);
 /* vec_cog_env<N>() (vec_environment.h:23-30): N default-constructed envs on `device`;
  * default params seed=std::random_device, 4 players, 3 pieces, EASY, 100000 max steps. */
 COG_API int cog_env_create(size_t n_envs, int device, cog_env **out);
+/* the same batch split over several GPUs of this process: shard k holds the contiguous envs
+ * [first_k, first_k + count_k), the reference ThreadedRunner's block split (runner.h:33-38:
+ * n / n_devices each, the last shard takes the remainder), with its own HIP stream.  A device
+ * may be listed more than once (two shards, two streams, one GPU).  Seeds are seed + global
+ * index, so every result is independent of the shard layout. */
+COG_API int cog_env_create_multi(size_t n_envs, const int *devices, int n_devices, cog_env **out);
+COG_API int cog_env_num_shards(const cog_env *env, int *out);
+COG_API int cog_env_shard_info(const cog_env *env, int shard, size_t *first, size_t *count, int *device);
 COG_API void cog_env_destroy(cog_env *env);
 COG_API int cog_env_num_envs(const cog_env *env, size_t *out);
 /* vec_cog_env::reset(seed, n_players, n_pieces, difficulty, max_steps, render)
@@ -110,15 +118,27 @@ COG_API int cog_env_reset_default(cog_env *env);
 /* vec_cog_env::step(actions) (vec_environment.h:46-61) with n == num_envs host ActionData
  * records; auto-resets finished envs; host views refreshed before return. */
 COG_API int cog_env_step(cog_env *env, const cog_action_t *actions, size_t n);
-/* same, actions already in device memory (e.g. a sampler's device actions) */
+/* same, actions already in device memory (e.g. a sampler's device actions); single-shard envs */
 COG_API int cog_env_step_device(cog_env *env, const void *d_actions, size_t n);
-/* views (allocates + fills the pinned host views on first use) */
+/* same, the actions produced by work queued on `stream` (a hipStream_t of the env's device, e.g.
+ * torch.cuda.current_stream()): the step is ordered after that work (event + stream wait) */
+COG_API int cog_env_step_device_stream(cog_env *env, const void *d_actions, size_t n, void *stream);
+/* views (allocates + fills the pinned host views on first use).  Device pointers are set for
+ * single-shard envs only; cog_env_shard_views gives shard k's device records and its slice of
+ * the host views. */
 COG_API int cog_env_get_views(cog_env *env, cog_env_views *out);
+COG_API int cog_env_shard_views(cog_env *env, int shard, cog_env_views *out);
 COG_API int cog_env_sync_host(cog_env *env);
 /* OR of hazard flags over envs; per_env (n entries) may be NULL */
 COG_API int cog_env_hazards(cog_env *env, uint32_t *flags_or, uint32_t *per_env);
 COG_API int cog_env_clear_hazards(cog_env *env);
-COG_API void *cog_env_stream(cog_env *env);     /* hipStream_t of the handle */
+COG_API void *cog_env_stream(cog_env *env);     /* hipStream_t of shard 0 */
+COG_API void *cog_env_shard_stream(cog_env *env, int shard);
+/* ordering against a caller's stream on shard k's device (e.g. torch.cuda.current_stream()):
+ * wait_stream: engine work queued later on shard k runs after the work queued on `stream` so far;
+ * signal_stream: work queued later on `stream` runs after the engine work queued on shard k */
+COG_API int cog_env_wait_stream(cog_env *env, int shard, void *stream);
+COG_API int cog_env_signal_stream(cog_env *env, int shard, void *stream);
 /* diagnostics: re-run the map-observation encode (map.cpp:389-405) over all envs `iters`
  * times back to back; average device time per launch (HIP events).  Output is unchanged.
  * variant: 0 = production kernel, >0 = alternative implementations kept for A/B timing. */
@@ -130,19 +150,25 @@ COG_API int cog_env_device(const cog_env *env); /* device ordinal */
 COG_API int cog_env_set_autoreset(cog_env *env, int on);
 
 /* ---- masked uniform random sampler ------------------------------------------------------- */
-/* vec_action_sampler<N>(seed) (vec_sampler.h:9-13): sampler i seeded seed + i (no u32 wrap). */
+/* vec_action_sampler<N>(seed) (vec_sampler.h:9-13): sampler i seeded seed + i (seed a u32, the
+ * sum not wrapped). */
 COG_API int cog_sampler_create(size_t n_envs, uint64_t seed, int device, cog_sampler **out);
+/* sharded like cog_env_create_multi (a runner needs the env's and the sampler's shards equal) */
+COG_API int cog_sampler_create_multi(size_t n_envs, uint64_t seed, const int *devices, int n_devices,
+                                     cog_sampler **out);
+COG_API int cog_sampler_num_shards(const cog_sampler *s, int *out);
 COG_API void cog_sampler_destroy(cog_sampler *s);
 /* vec_action_sampler::sample(masks) (vec_sampler.h:14-21): n == num_envs host ActionMask
  * records; host actions view refreshed before return. */
 COG_API int cog_sampler_sample(cog_sampler *s, const cog_action_mask_t *masks, size_t n);
-/* same, masks in device memory (e.g. an env's d_selected_action_masks) */
+/* same, masks in device memory (e.g. an env's d_selected_action_masks); single-shard samplers */
 COG_API int cog_sampler_sample_device(cog_sampler *s, const void *d_masks, size_t n);
 COG_API cog_action_t *cog_sampler_actions(cog_sampler *s);   /* persistent host view */
-COG_API void *cog_sampler_device_actions(cog_sampler *s);    /* device view */
+COG_API void *cog_sampler_device_actions(cog_sampler *s);    /* device view (shard 0) */
+COG_API void *cog_sampler_shard_device_actions(cog_sampler *s, int shard);
 COG_API int cog_sampler_device(const cog_sampler *s);       /* device ordinal */
 
-/* ---- runner: asynchronous sample/step on the env's stream (runner.h:81-100) ----------------- */
+/* ---- runner: asynchronous sample/step on the env's streams (runner.h:81-100) ---------------- */
 COG_API int cog_runner_create(cog_env *env, cog_sampler *s, size_t n_threads, uint32_t flags,
                               cog_runner **out);
 COG_API void cog_runner_destroy(cog_runner *r);
@@ -156,7 +182,8 @@ COG_API int cog_runner_rollout(cog_runner *r, int steps);   /* enqueue steps x (
 COG_API int cog_runner_set_chunk(cog_runner *r, int steps_per_launch);
 COG_API int cog_runner_set_timing(cog_runner *r, int enable);
 /* device time of the fused launches since enabled: HIP events bracket each step() launch and each
-   rollout() batch on the env's stream; *launches = fused launches covered */
+   rollout() batch on every shard's stream; the slowest shard's total; *launches = fused launches
+   covered */
 COG_API int cog_runner_kernel_time(cog_runner *r, double *total_ms, uint64_t *launches);
 
 #ifdef __cplusplus

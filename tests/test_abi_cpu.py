@@ -55,10 +55,10 @@ def test_python_surface(cg):
 
 
 def test_dtypes_match_reference_layout(cg):
-    assert cg.ObsData == po.OBS and cg.ActionMask == po.MASK
-    assert cg.ActionData == po.ACTION and cg.Info == po.INFO
-    assert cg.ObsData.itemsize == 17216 and cg.ActionMask.itemsize == 128
-    assert cg.ObsData["player_data"].base["action_mask"]["play"] == np.dtype(("?", (22,)))
+    assert np.dtype(cg.ObsData) == po.OBS and np.dtype(cg.ActionMask) == po.MASK
+    assert np.dtype(cg.ActionData) == po.ACTION and np.dtype(cg.Info) == po.INFO
+    assert cg.ObsData.dtype.itemsize == 17216 and cg.ActionMask.dtype.itemsize == 128
+    assert cg.ObsData.dtype["player_data"].base["action_mask"]["play"] == np.dtype(("?", (22,)))
 
 
 def test_no_gpu_fails_loudly(cg):

@@ -1,0 +1,140 @@
+"""GPU: the BASELINE configurations at their own sizes (BASELINE.json configs),
+against the C oracle on the same seeds.  The engine's wave-uniform fast paths (the play/pass
+short path, the narrow/wide deck ballot, the sampler's head ballot) depend on which envs share
+a wave, so the configs run at the sizes they are quoted on.  Bit-exact over named fields.
+
+  C2          n=256, 4p, EASY: 10,000 selected-mask steps through the runner's device loop, all
+              256 envs checked at checkpoints; and 1,000 steps of the reference's host loop
+              (sampler.sample(masks); env.step(actions)) with every env checked every step
+  C4 shard    n=8,192, 4p, HARD (the last of the 8 shards of 65,536: start piece B region), host
+              views refreshed every step by runner.sample(); runner.step_sync(), all envs checked
+  full dyn.   stored-mask driver (moves, shop, specials) with auto-resets and device map
+              generation inside the rollout: all 8,192 envs of a C3-size batch (MEDIUM), and 256
+              envs of a C5-size batch (65,536, HARD) against 1-env-per-seed oracle runs
+"""
+import numpy as np
+import pytest
+
+import pyoracle as po
+
+pytestmark = pytest.mark.gpu
+FIELDS = ("observations", "selected_action_masks", "infos")
+
+
+def assert_equal(env, orc, lo=0, hi=None, what=""):
+    hi = env.agent_selection.shape[0] if hi is None else hi
+    for nm in FIELDS:
+        bad = po.named_equal(getattr(env, nm)[lo:hi], getattr(orc, nm))
+        assert bad is None, f"{what}: {nm}.{bad} differs from the oracle"
+    for nm in ("rewards", "dones", "agent_selection"):
+        assert np.array_equal(getattr(env, nm)[lo:hi], getattr(orc, nm)), f"{what}: {nm} differs"
+
+
+def test_C2_n256_easy_rollout_10000_steps(cg):
+    n, seed, steps, every = 256, 12345, 10000, 1000
+    env = cg.vec.get_vec_env(n)()
+    smp = cg.vec.get_vec_sampler(n)(seed)
+    env.reset(seed, 4, 3, cg.EASY, 100000, False)
+    runner = cg.vec.get_runner(n)(env, smp, None, device_views=True)
+    runner.set_chunk(250)
+    orc, osm = po.OracleVec(n), po.OracleSampler(n, seed)
+    orc.reset(seed, 4, 3, 0, 100000)
+    for t in range(0, steps, every):
+        runner.rollout(every)
+        runner.sync()
+        env.sync_host()
+        for _ in range(every):
+            osm.sample(orc.selected_action_masks)
+            orc.step(osm.actions)
+        assert_equal(env, orc, what=f"C2 step {t + every}")
+    assert np.array_equal(env.hazards()[1], orc.flags())
+
+
+def test_C2_n256_easy_host_loop_every_step(cg):
+    n, seed = 256, 777
+    env = cg.vec.get_vec_env(n)()
+    smp = cg.vec.get_vec_sampler(n)(seed)
+    env.reset(seed, 4, 3, cg.EASY, 100000, False)
+    orc, osm = po.OracleVec(n), po.OracleSampler(n, seed)
+    orc.reset(seed, 4, 3, 0, 100000)
+    masks, acts = env.selected_action_masks, smp.get_actions()
+    for t in range(1000):
+        smp.sample(masks)
+        env.step(acts)
+        osm.sample(orc.selected_action_masks)
+        orc.step(osm.actions)
+        assert po.named_equal(acts, osm.actions) is None, f"C2 host loop: actions differ at step {t}"
+        assert_equal(env, orc, what=f"C2 host loop step {t}")
+
+
+def test_C4_shard_n8192_hard_host_views_every_step(cg):
+    from city_of_gold.shard import shard, shard_seed
+    lo, hi = shard(65536, 7, 8)                            # the 8th GPU's shard of C4
+    n, base = hi - lo, shard_seed(12345, lo)
+    env = cg.vec.get_vec_env(n)()
+    smp = cg.vec.get_vec_sampler(n)(base)
+    env.reset(base, 4, 3, cg.HARD, 100000, False)
+    runner = cg.vec.get_runner(n)(env, smp, 8)
+    orc, osm = po.OracleVec(n), po.OracleSampler(n, base)
+    orc.reset(base, 4, 3, 2, 100000)
+    acts = runner.get_actions()
+    sub = slice(0, n, 37)                                  # a strided subset checked every step
+    for t in range(1, 201):
+        runner.sample()
+        runner.step_sync()
+        osm.sample(orc.selected_action_masks)
+        orc.step(osm.actions)
+        assert po.named_equal(acts[sub], osm.actions[sub]) is None, f"C4 shard actions step {t}"
+        for nm in ("selected_action_masks", "infos"):
+            assert po.named_equal(getattr(env, nm)[sub], getattr(orc, nm)[sub]) is None, f"C4 shard {nm} step {t}"
+        for f in ("phase", "current_resources", "shop"):
+            assert np.array_equal(env.observations["shared"][f][sub], orc.observations["shared"][f][sub]), (f, t)
+        if t % 50 == 0:
+            assert_equal(env, orc, what=f"C4 shard step {t}")
+    starts = orc.observations["shared"]["map"][:, :, :, 6].reshape(n, -1).sum(1)
+    assert starts.min() > 0                                # every env has its end hexes
+
+
+def test_full_dynamics_resets_C3_size_all_envs(cg):
+    n, seed, steps = 8192, 4242, 240
+    env = cg.vec.get_vec_env(n)()
+    smp = cg.vec.get_vec_sampler(n)(seed)
+    env.reset(seed, 4, 3, cg.MEDIUM, 30, False)
+    runner = cg.vec.get_runner(n)(env, smp, None, device_views=True, stored_masks=True)
+    runner.set_chunk(60)
+    runner.rollout(steps)
+    runner.sync()
+    env.sync_host()
+    orc, osm = po.OracleVec(n), po.OracleSampler(n, seed)
+    orc.reset(seed, 4, 3, 1, 30)
+    resets = 0
+    for _ in range(steps):
+        osm.sample(po.stored_masks(orc))
+        orc.step(osm.actions)
+        resets += int(orc.dones.sum())
+    assert resets > n // 2                                 # auto-resets happened inside launches
+    assert_equal(env, orc, what="C3-size full dynamics")
+    assert np.array_equal(env.hazards()[1], orc.flags())
+
+
+@pytest.mark.parametrize("block", [(0, 128), (65536 - 128, 65536)], ids=["first128", "last128"])
+def test_full_dynamics_resets_C5_size_subsets(cg, block):
+    n, seed, steps = 65536, 90001, 200
+    env = cg.vec.get_vec_env(n)()
+    smp = cg.vec.get_vec_sampler(n)(seed)
+    env.reset(seed, 4, 3, cg.HARD, 30, False)
+    runner = cg.vec.get_runner(n)(env, smp, None, device_views=True, stored_masks=True)
+    runner.set_chunk(100)
+    runner.rollout(steps)
+    runner.sync()
+    env.sync_host()
+    lo, hi = block
+    orc, osm = po.OracleVec(hi - lo), po.OracleSampler(hi - lo, seed + lo)
+    orc.reset(seed + lo, 4, 3, 2, 30)                      # env i == a batch seeded seed + i
+    resets = 0
+    for _ in range(steps):
+        osm.sample(po.stored_masks(orc))
+        orc.step(osm.actions)
+        resets += int(orc.dones.sum())
+    assert resets > (hi - lo) // 2
+    assert_equal(env, orc, lo, hi, what=f"C5-size full dynamics envs [{lo}, {hi})")

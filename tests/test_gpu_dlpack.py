@@ -63,3 +63,48 @@ def test_step_device_equals_host_step(cg):
         a.sync_host()
         for nm in ("observations", "selected_action_masks", "infos"):
             assert np.array_equal(getattr(a, nm).view(np.uint8), getattr(b, nm).view(np.uint8)), nm
+
+
+def test_step_device_orders_after_torch_stream(cg):
+    """No torch.cuda.synchronize(): the actions are written on torch's current stream behind a
+    long matmul chain, then step_device() is called at once; it must order its kernel after that
+    stream (event + stream wait), not read the tensor's old (all-pass) contents."""
+    import torch
+    n = 4096
+    a, _ = make(cg, n, 9)
+    b, _ = make(cg, n, 9)
+    masks = a.selected_action_masks.view(np.uint8).reshape(n, 128)[:, :22].astype(bool)
+    acts = np.zeros(n, dtype=cg.ActionData)
+    acts["play"] = np.where(masks[:, 1:].any(1), masks[:, 1:].argmax(1) + 1, 0).astype(np.uint8)
+    assert (acts["play"] > 0).sum() > n // 2
+    src = torch.from_numpy(acts.view(np.uint8).reshape(n, 64).copy()).pin_memory()
+    d_acts = torch.zeros((n, 64), dtype=torch.uint8, device="cuda")
+    m = torch.randn(4096, 4096, device="cuda")
+    torch.cuda.synchronize()
+    for _ in range(30):                                    # ~tens of ms of work on torch's stream
+        m = torch.tanh(m @ m)
+    d_acts.copy_(src, non_blocking=True)                  # queued behind the matmuls
+    a.step_device(d_acts.data_ptr())                      # orders after torch's current stream
+    b.step(acts)
+    for nm in ("observations", "selected_action_masks", "infos"):
+        assert np.array_equal(getattr(a, nm).view(np.uint8), getattr(b, nm).view(np.uint8)), nm
+    del m
+
+
+def test_signal_stream_orders_torch_reads_after_rollout(cg):
+    """A device-views rollout is asynchronous; env.signal_stream(torch stream) makes torch's
+    later reads wait for it without runner.sync()."""
+    import torch
+    n = 4096
+    env, smp = make(cg, n, 13)
+    runner = cg.vec.get_runner(n)(env, smp, None, device_views=True)
+    runner.set_chunk(1000)
+    t = cg.device_tensors(env)
+    runner.rollout(3000)                                   # milliseconds of device work
+    env.signal_stream(cg.stream_handle())
+    snap = t["selected_action_masks"].clone()              # on torch's stream, after the rollout
+    dn = t["infos"].clone()
+    runner.sync()
+    env.sync_host()
+    assert np.array_equal(snap.cpu().numpy(), env.selected_action_masks.view(np.uint8).reshape(n, -1))
+    assert np.array_equal(dn.cpu().numpy(), env.infos.view(np.uint8).reshape(n, -1))

@@ -101,3 +101,48 @@ def test_natural_end_and_dead_steps(cg):
         orc.step(osm.actions)
         assert po.named_equal(obs, orc.observations) is None, f"step {t}"
         assert po.named_equal(mask, orc.selected_action_masks) is None, f"step {t}"
+
+
+def test_reference_unit_loop_with_record_classes(cg):
+    """test_environment.cpp:83-102 verbatim in Python: the record classes (single_env.cpp:34-85),
+    action_sampler() with its default seed 42 (common.cpp:25-27, sampler.h:9-12) on the acting
+    player's stored mask, cog_env.init() binding the records."""
+    sampler = cg.action_sampler()
+    observation, mask, info = cg.ObsData(), cg.ActionMask(), cg.Info()
+    rewards = np.zeros(4, dtype=np.float32)
+    assert mask.play[0] and not mask.play[1:].any() and mask.move[0]     # ActionMask() defaults
+    env = cg.cog_env()
+    env.init(observation, info, rewards, mask)
+    env.reset(54321, 4, 5, cg.MEDIUM, 100, False)
+    steps = 0
+    while True:
+        current_agent = env.agent_selection
+        act = sampler.sample(observation.player_data[current_agent].action_mask)
+        assert isinstance(act, cg.ActionData)
+        env.step(act)
+        steps += 1
+        if env.get_done():
+            break
+    assert env.get_info().total_length == 100 and steps == 499
+    assert info["total_length"] == 100                     # the bound record was updated
+    assert observation.shared.map.shape == (48, 48, 7) and observation.shared.phase in (0, 1, 2)
+    assert len(observation.player_data) == 4
+    deck = observation.player_data[0].obs
+    assert int(deck.draw.sum() + deck.hand.sum() + deck.active.sum() + deck.discard.sum()) >= 8
+
+
+def test_action_sampler_matches_vec_sampler(cg):
+    """action_sampler(seed).sample(mask) == vec_sampler(1)(seed) on the same masks."""
+    rng = np.random.default_rng(1)
+    a, v = cg.action_sampler(99), cg.vec.get_vec_sampler(1)(99)
+    for _ in range(50):
+        m = cg.ActionMask()
+        for head, k in (("play", 22), ("play_special", 22), ("remove", 22), ("move", 7), ("get_from_shop", 19)):
+            bits = rng.random(k) < 0.3
+            bits[0] = True
+            setattr(m, head, bits)
+        act = a.sample(m)
+        v.sample(m.record.reshape(1))
+        assert act == v.get_actions()[0]
+        rec = cg.ActionData(play=act.play)
+        assert rec.play == act.play and np.dtype(cg.ActionData).itemsize == 64

@@ -1,17 +1,17 @@
 #!/bin/bash
-# PMC passes over the benchmark workload (bench.py --profile-steps): each counter group in its own
-# rocprofv3 run with --kernel-trace only (never combined with sys/runtime traces), then a
-# per-kernel summary.   Usage (on the GPU box): tools/pmc_passes.sh TAG [steps]
+# PMC passes over the benchmark workload (bench.py --profile-steps K): each counter group in its
+# own rocprofv3 run with --kernel-trace only (never combined with sys/runtime traces), then a
+# per-kernel summary.   Usage (on the GPU box): tools/pmc_passes.sh TAG [K] [chunk]
 set -o pipefail
-TAG=${1:-pmc}; STEPS=${2:-200}
+TAG=${1:-pmc}; STEPS=${2:-2000}; CHUNK=${3:-1000}
 OUT=$PWD/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 BENCH="$PWD/bench.py"
 run() {   # name, counters...
   local name=$1; shift
-  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/$name" -o run \
-      --pmc "$@" -- python3 "$BENCH" --profile-steps "$STEPS" --warmup 0 --no-cpu-baseline) \
+  (cd /tmp && timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d "$OUT/$name" -o run \
+      --pmc "$@" -- python3 "$BENCH" --profile-steps "$STEPS" --chunk "$CHUNK" --warmup 0 --no-cpu-baseline) \
       > "$OUT/$name.log" 2>&1
 }
 run sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS && \

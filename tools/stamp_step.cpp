@@ -28,7 +28,7 @@ int main(int argc, char **argv) {
     constexpr int K = 16;
     if (hipMalloc(&d, waves * K * sizeof(unsigned long long)) != hipSuccess) return 1;
     if (hipMemset(d, 0, waves * K * sizeof(unsigned long long)) != hipSuccess) return 1;
-    env->s.stamps = d;
+    env->sh[0].s.stamps = d;
     cog_runner_set_chunk(run, chunk);
     cog_runner_rollout(run, chunk);
     cog_runner_sync(run);
@@ -55,7 +55,7 @@ int main(int argc, char **argv) {
   constexpr int K = 16;
   unsigned long long *d;
   if (hipMalloc(&d, waves * K * sizeof(unsigned long long)) != hipSuccess) return 1;
-  env->s.stamps = d;
+  env->sh[0].s.stamps = d;
   std::vector<unsigned long long> h(waves * K);
   // phase j = ticks from the previous stamp that was reached to stamp j
   const char *names[K] = {"", "loads (2 rounds) + sample + unpack", "repack registers",
