@@ -72,8 +72,11 @@ def _make_env_cls(n):
 
     def step_device(self, d_actions, stream=None):
         """step() with ActionData records in device memory (a torch tensor's data_ptr()),
-        ordered after torch's current stream unless `stream` (a handle, 0: none) is given."""
-        _C.VecEnvBase.step_device(self, d_actions, stream_handle() if stream is None else int(stream))
+        ordered after torch's current stream, or after `stream` (a hipStream_t handle, 0 = the
+        null stream; -1: no ordering)."""
+        if stream is None:
+            stream = stream_handle()
+        _C.VecEnvBase.step_device(self, d_actions, -1 if stream is None else int(stream))
 
     doc = (f"Vectorized city of gold environment for {n} environments.\n\n"
            "reset() must be called first to initialize the environments before stepping.")
@@ -133,15 +136,16 @@ def device_tensors(env, sampler=None, shard=0):
 
 
 def stream_handle(device=None):
-    """torch's current HIP stream on `device` as an int handle (0 without torch), the stream
-    argument of step_device / wait_stream / signal_stream."""
+    """torch's current HIP stream on `device` as an int handle (0 is the null stream, torch's
+    default), the stream argument of step_device / wait_stream / signal_stream; None without
+    torch."""
     try:
         import torch
         if torch.cuda.is_available():
             return int(torch.cuda.current_stream(device).cuda_stream)
     except Exception:
         pass
-    return 0
+    return None
 
 
 from .single import cog_env  # noqa: E402  (src/pybind/single_env.cpp: the single-env API)

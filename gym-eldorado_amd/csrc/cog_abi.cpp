@@ -515,8 +515,8 @@ int cog_env_step_device_stream(cog_env *env, const void *d_actions, size_t n, vo
   DeviceGuard g(k.device);
   int rc = prepare_host(env);
   if (rc) return rc;
-  if (stream) {                       // the caller's stream produced the actions: order after it
-    HIPCHK(hipEventRecord(k.ev, static_cast<hipStream_t>(stream)));
+  if (stream != COG_NO_STREAM) {      // the caller's stream produced the actions: order after it
+    HIPCHK(hipEventRecord(k.ev, static_cast<hipStream_t>(stream)));   // (NULL: the null stream)
     HIPCHK(hipStreamWaitEvent(k.stream, k.ev, 0));
   }
   if (cog::launch_step(launch_state(k, env->host), static_cast<const uint8_t *>(d_actions), k.stream))
@@ -525,7 +525,7 @@ int cog_env_step_device_stream(cog_env *env, const void *d_actions, size_t n, vo
 }
 
 int cog_env_step_device(cog_env *env, const void *d_actions, size_t n) {
-  return cog_env_step_device_stream(env, d_actions, n, nullptr);
+  return cog_env_step_device_stream(env, d_actions, n, COG_NO_STREAM);
 }
 
 int cog_env_step(cog_env *env, const cog_action_t *actions, size_t n) {

@@ -1461,9 +1461,8 @@ DEV void dup_sink(const RegEnv &R2) {
 DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i, int na PH_PARAM) {
   const int ag = (int)R.agent();
   PState &P = R.P;
-  const uint32_t info = ((R.info_steps >> (8 * ag)) + 1u) & 0xffu;   // Info steps_taken (u8)
-  R.info_steps = (R.info_steps & ~(0xffu << (8 * ag))) | (info << (8 * ag));
-  s.info[i * COG_INFO_BYTES + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag] = (uint8_t)info;
+  const uint32_t info = ((R.info_steps >> (8 * ag)) + 1u) & 0xffu;   // Info steps_taken (u8):
+  R.info_steps = (R.info_steps & ~(0xffu << (8 * ag))) | (info << (8 * ag));   // stored with the outputs
   uint32_t phase = R.sh[0] & 0xffu;
   if (phase == COG_PHASE_INACTIVE) phase = COG_PHASE_MOVEMENT;
   P.steps_taken = (P.steps_taken + 1) & 0xffu;
@@ -1645,7 +1644,10 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
   R.sh[0] = (R.sh[0] & ~0xffu) | phase;
   R.sh[1] = __float_as_uint(r0); R.sh[2] = __float_as_uint(r1); R.sh[3] = __float_as_uint(r2);
 #ifndef COG_ABLATE_ROWS                                    // diagnostic timing builds only
-  if (!wave_simple) rows_ready(moved_rows);               // (uniform: converged)
+  // on every path, converged: the wait for the rows then sits where no store of this step is
+  // outstanding yet (the step's stores all come after it), and no later reuse of the row
+  // registers needs a conservative vmcnt wait -- which would wait for this step's stores
+  rows_ready(moved_rows);
 #endif
   if (!wave_simple && R.moved) {                           // the mover's new neighbourhood
     R.cells_a = cells_from_rows(moved_rows, R.g2);
@@ -1760,6 +1762,7 @@ DEV void store_mask_record(uint4 *rec, const MBits &b, uint32_t gm) {
 // A move stores the new locations at once: the next move re-reads them.
 DEV void store_outputs(const DevState &s, size_t i, int ag, int na, const Snap &S, const RegEnv &R) {
   uint8_t *ob = s.obs + i * COG_OBS_BYTES;
+  s.info[i * COG_INFO_BYTES + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag] = (uint8_t)(R.info_steps >> (8 * ag));
   if (R.moved) reinterpret_cast<uint4 *>(s.priv + i)[2] = R.g2;
 #pragma unroll
   for (int k = 0; k < 3; k++) {
@@ -1865,16 +1868,16 @@ DEV bool env_step_lane(const DevState &s, size_t i, const uint8_t *act_in, uint3
   if (SRC == MASK_SELECTED) step_action<SRC>(R, act_in, i, srng, act);
   regs_players(R, S);
   if (SRC != MASK_SELECTED) step_action<SRC>(R, act_in, i, srng, act);
-  if (SRC != MASK_EXTERNAL) {
-    rngs[i] = srng;
-    store_action(actions_out + i * COG_ACTION_BYTES, act);
-  }
   STAMP(s, 1);
   const bool was_done = R.done() != 0u;
   const bool finish = !was_done && step_regs(R, act, s, i, na PH_PASS);
   if (finish) R.set_done(1u);
   STAMP(s, 2);
   store_changes(s, i, ag, na, S, R);
+  if (SRC != MASK_EXTERNAL) {                              // (every store after the step's loads)
+    rngs[i] = srng;
+    store_action(actions_out + i * COG_ACTION_BYTES, act);
+  }
   STAMP(s, 3);
   uint32_t agent = R.agent(), out = ~0u;
   const bool enc = end_of_step(s, i, was_done, finish, agent, out);
@@ -1988,6 +1991,10 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s, int steps, uint32_t
     const int ag = (int)(S.g1.y & 0xffu);
     lds_players(L, l, ag, next_of(ag), S);
   }
+  // Every load above completes before the loop: the loop issues no load whose wait could be
+  // merged with them, so the wait-count pass places no per-iteration vmcnt wait for registers
+  // they wrote (such a wait, executed every step, would also wait for the step's stores).
+  __builtin_amdgcn_s_waitcnt(0);
   PH_DECL;
   for (int t = FIX ? 1 : 0; t < steps; t++) {
     if (!FIX && !live) break;                              // lean: a parked lane leaves the loop
@@ -2010,7 +2017,6 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s, int steps, uint32_t
 #endif
       regs_players(R, S);
       if (SRC == MASK_STORED) step_action<SRC>(R, nullptr, i, srng, act);
-      store_action(actions_out + i * COG_ACTION_BYTES, act);
       PH(1);
       const bool was_done = R.done() != 0u;
       const bool finish = !was_done && step_regs(R, act, s, i, na PH_PASS);
@@ -2018,6 +2024,7 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s, int steps, uint32_t
       PH(2);
 #ifndef COG_ABLATE_STORES                                  // diagnostic timing builds only
       store_outputs(s, i, ag, na, S, R);
+      store_action(actions_out + i * COG_ACTION_BYTES, act);
 #endif
       PH(3);
       // the next step's image: registers (env level) and this wave's LDS (player level)

@@ -403,12 +403,13 @@ PYBIND11_MODULE(_city_of_gold, m) {
         if (name == "infos") return dl_capsule(v.d_infos, dev, n, sizeof(Info), kDLUInt, 8, self);
         throw py::value_error("no device view named " + name);
       }, "name"_a, "shard"_a = 0)
-      .def("step_device", [](VecEnv &e, uintptr_t d_actions, uintptr_t stream) {
+      .def("step_device", [](VecEnv &e, uintptr_t d_actions, int64_t stream) {
         // step with ActionData records already in device memory (e.g. a torch tensor's data_ptr()),
-        // ordered after the work queued on `stream` (0: none)
+        // ordered after the work queued on `stream` (a hipStream_t handle, 0 = the null stream;
+        // -1: no ordering)
         check(cog_env_step_device_stream(e.handle(), reinterpret_cast<const void *>(d_actions), e.num_envs(),
-                                         reinterpret_cast<void *>(stream)));
-      }, "d_actions"_a, "stream"_a = 0)
+                                         stream < 0 ? COG_NO_STREAM : reinterpret_cast<void *>((uintptr_t)stream)));
+      }, "d_actions"_a, "stream"_a = -1)
       .def("wait_stream", [](VecEnv &e, uintptr_t stream, int k) {
         check(cog_env_wait_stream(e.handle(), k, reinterpret_cast<void *>(stream)));
       }, "stream"_a, "shard"_a = 0)

@@ -121,7 +121,9 @@ COG_API int cog_env_step(cog_env *env, const cog_action_t *actions, size_t n);
 /* same, actions already in device memory (e.g. a sampler's device actions); single-shard envs */
 COG_API int cog_env_step_device(cog_env *env, const void *d_actions, size_t n);
 /* same, the actions produced by work queued on `stream` (a hipStream_t of the env's device, e.g.
- * torch.cuda.current_stream()): the step is ordered after that work (event + stream wait) */
+ * torch.cuda.current_stream(); NULL is the null stream): the step is ordered after that work
+ * (event + stream wait).  COG_NO_STREAM: no ordering (cog_env_step_device). */
+#define COG_NO_STREAM ((void *)(intptr_t)-1)
 COG_API int cog_env_step_device_stream(cog_env *env, const void *d_actions, size_t n, void *stream);
 /* views (allocates + fills the pinned host views on first use).  Device pointers are set for
  * single-shard envs only; cog_env_shard_views gives shard k's device records and its slice of
@@ -134,7 +136,8 @@ COG_API int cog_env_hazards(cog_env *env, uint32_t *flags_or, uint32_t *per_env)
 COG_API int cog_env_clear_hazards(cog_env *env);
 COG_API void *cog_env_stream(cog_env *env);     /* hipStream_t of shard 0 */
 COG_API void *cog_env_shard_stream(cog_env *env, int shard);
-/* ordering against a caller's stream on shard k's device (e.g. torch.cuda.current_stream()):
+/* ordering against a caller's stream on shard k's device (e.g. torch.cuda.current_stream();
+ * NULL is the null stream):
  * wait_stream: engine work queued later on shard k runs after the work queued on `stream` so far;
  * signal_stream: work queued later on `stream` runs after the engine work queued on shard k */
 COG_API int cog_env_wait_stream(cog_env *env, int shard, void *stream);
