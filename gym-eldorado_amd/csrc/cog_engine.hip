@@ -91,6 +91,26 @@ __constant__ int8_t c_opts_range[6] = {-2, -1, 0, 1, 2, 3};
 __constant__ int8_t c_opts_ls[2] = {-1, 2};
 __constant__ int8_t c_opts_lt[1] = {-3};
 
+// the uniform's division table (cog_rng.h uid_entry): constant memory, copied to LDS by each
+// kernel that draws (a per-lane k indexes it)
+struct UidTab {
+  UidEntry e[kUidTab];
+};
+constexpr UidTab make_uid_tab() {
+  UidTab t{};
+  for (int k = 0; k < kUidTab; k++) t.e[k] = uid_entry((uint32_t)k);
+  return t;
+}
+__constant__ UidTab c_uid_tab = make_uid_tab();
+DEV void uid_tab_fill(UidEntry *lds) {                    // the first 32 work-items; then a barrier
+  if (threadIdx.x < (unsigned)kUidTab) lds[threadIdx.x] = c_uid_tab.e[threadIdx.x];
+  __syncthreads();
+}
+DEV uint32_t uid_tab(const UidEntry *tab, uint32_t r, uint32_t k) {   // k in [1, 31], r accepted
+  const UidEntry e = tab[k];
+  return uid_tab_accepted(r, e.s, e.m);
+}
+
 // shop slots that start in the market (cards.cpp:85-92 / 94-100): slots 0,1,5,7,9,12
 constexpr uint32_t kInMarket0 = (1u << 0) | (1u << 1) | (1u << 5) | (1u << 7) | (1u << 9) | (1u << 12);
 
@@ -889,10 +909,12 @@ DEV uint8_t pick(uint32_t &rng, uint32_t m) {
 // branch-free first (the state advances past a head only if it has candidates), and only the
 // heads with two or more candidates do arithmetic.  A lane holding a draw that might be rejected
 // (probability < 2^-25 per head) redoes the sampling the sequential way, rejections included.
-DEV void sample_heads(const Heads &h, uint32_t &rng, uint8_t out[5]) {
+DEV void sample_heads(const Heads &h, uint32_t &rng, uint8_t out[5], const UidEntry *tab) {
   const uint32_t m[5] = {h.play, h.spec, h.rem, h.move, h.shop};
   uint32_t x = rng, r[5], k[5];
   bool risk = false;
+  const UidEntry e0 = tab[__popc(m[0])];                  // head 0's entry, read before the draws
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int j = 0; j < 5; j++) {
     k[j] = __popc(m[j]);
@@ -901,6 +923,7 @@ DEV void sample_heads(const Heads &h, uint32_t &rng, uint8_t out[5]) {
     x = k[j] ? xn : x;
     risk |= k[j] != 0u && r[j] >= kSmallSafe;
   }
+  __builtin_amdgcn_sched_barrier(0);
   if (risk) {
     uint32_t y = rng;
 #pragma unroll
@@ -911,17 +934,17 @@ DEV void sample_heads(const Heads &h, uint32_t &rng, uint8_t out[5]) {
   rng = x;
 #pragma unroll
   for (int j = 0; j < 5; j++) out[j] = (uint8_t)(k[j] ? (uint32_t)(__ffs(m[j]) - 1) : 0u);
-  if (k[0] >= 2u) out[0] = (uint8_t)nth_set_bit(m[0], uid_small_accepted(r[0], k[0]));
+  if (k[0] >= 2u) out[0] = (uint8_t)nth_set_bit(m[0], uid_tab_accepted(r[0], e0.s, e0.m));
   // heads 1-4 rarely hold two candidates (the selected mask's special / remove / move / shop
   // heads): one uniform branch skips them all when no lane of the wave needs arithmetic there
   if (__builtin_amdgcn_ballot_w64(max(max(k[1], k[2]), max(k[3], k[4])) >= 2u)) {
 #pragma unroll
     for (int j = 1; j < 5; j++)
-      if (k[j] >= 2u) out[j] = (uint8_t)nth_set_bit(m[j], uid_small_accepted(r[j], k[j]));
+      if (k[j] >= 2u) out[j] = (uint8_t)nth_set_bit(m[j], uid_tab(tab, r[j], k[j]));
   }
 }
-DEV void sample_mask(const uint8_t *mask, uint32_t &rng, uint8_t out[5]) {
-  sample_heads(heads_of(mbits_from_bytes(mask)), rng, out);
+DEV void sample_mask(const uint8_t *mask, uint32_t &rng, uint8_t out[5], const UidEntry *tab) {
+  sample_heads(heads_of(mbits_from_bytes(mask)), rng, out, tab);
 }
 DEV void store_action(uint8_t *dst, const uint8_t a[5]) {
   const uint32_t lo = (uint32_t)a[0] | (uint32_t)a[1] << 8 | (uint32_t)a[2] << 16 | (uint32_t)a[3] << 24;
@@ -1068,6 +1091,7 @@ struct RegEnv {
   bool moved;
   uint4 g2;                                                // map bounds + locations
   uint32_t avail;                                          // shop_avail(), kept across steps
+  const UidEntry *tab;                                     // the uniform's table (LDS)
 
   DEV uint32_t n_players() const { return g1x & 0xffu; }
   DEV uint32_t done() const { return g1x >> 24; }
@@ -1186,13 +1210,14 @@ struct RegEnv {
     P.n_in_hand = (P.n_in_hand + n) & 0xffu;
   }
   template <int NQ>
-  DEV void draw_fast(uint32_t pre[6], uint32_t n, uint32_t K0, const uint32_t xs[COG_HAND_SIZE]) {
+  DEV void draw_fast(uint32_t pre[6], uint32_t n, uint32_t K0, const uint32_t xs[COG_HAND_SIZE],
+                     const UidEntry ue[COG_HAND_SIZE]) {
     constexpr uint32_t NT = NQ < 6 ? 4 * NQ : COG_N_CARDTYPES;   // types covered
     uint32_t dm = 0;                                     // types drawn
 #pragma unroll
     for (int j = 0; j < COG_HAND_SIZE; j++) {
       const uint32_t live = (uint32_t)j < n ? 0x80808080u : 0u;
-      const uint32_t T = bcast8(uid_small_accepted(xs[j] - 1u, max(K0 - (uint32_t)j, 1u)) + 1u);
+      const uint32_t T = bcast8(uid_tab_accepted(xs[j] - 1u, ue[j].s, ue[j].m) + 1u);
       uint32_t above = 0;                                // as below
 #pragma unroll
       for (int q = 0; q < NQ; q++) {
@@ -1202,7 +1227,11 @@ struct RegEnv {
       }
       dm |= live ? 1u << (NT - above) : 0u;
     }
-    if (n) rng = n == 1u ? xs[0] : n == 2u ? xs[1] : n == 3u ? xs[2] : xs[3];
+    uint32_t x = rng;                                      // the state after the n-th draw: selects,
+    x = n >= 1u ? xs[0] : x;                               // no branches
+    x = n >= 2u ? xs[1] : x;
+    x = n >= 3u ? xs[2] : x;
+    rng = n >= 4u ? xs[3] : x;
     P.n_in_draw = (K0 - n) & 0xffu;
     draw_rebuild<NQ>(pre, dm);
   }
@@ -1225,16 +1254,21 @@ struct RegEnv {
     // value below kSmallSafe (no rejection for any pile of <= 31) they are the states the
     // sequential draws reach, and the n uniforms need no serial chain.  n <= COG_HAND_SIZE.
     const uint32_t K0 = P.n_in_draw;
-    uint32_t xs[COG_HAND_SIZE];
+    UidEntry ue[COG_HAND_SIZE];                            // the draws' table entries, read first:
+#pragma unroll                                             // the LDS reads overlap the jumps below
+    for (int j = 0; j < COG_HAND_SIZE; j++) ue[j] = tab[min(max(K0 - (uint32_t)j, 1u), 31u)];
+    __builtin_amdgcn_sched_barrier(0);                     // (kept ahead of the jumps: the
+    uint32_t xs[COG_HAND_SIZE];                            // scheduler sinks loads to their use)
     bool seq = K0 > 31u || n > (uint32_t)COG_HAND_SIZE;
 #pragma unroll
     for (int j = 0; j < COG_HAND_SIZE; j++) {
       xs[j] = mr_jump(rng, mr_pow(j + 1));
       seq |= (uint32_t)j < n && xs[j] - 1u >= kSmallSafe;
     }
+    __builtin_amdgcn_sched_barrier(0);
     const bool fast = total == P.n_in_draw && total < 128u && !seq;
     if (fast) {
-      draw_fast<NQ>(pre, n, K0, xs);
+      draw_fast<NQ>(pre, n, K0, xs, ue);
     } else if (total == P.n_in_draw && total < 128u) {     // every prefix sum fits in 7 bits
       uint32_t dm = 0;                                     // types drawn
       for (uint32_t i = 0; i < n; i++) {
@@ -1804,8 +1838,8 @@ DEV void store_changes(const DevState &s, size_t i, int ag, int na, const Snap &
 // reference's out-of-range accesses: clamped and flagged)
 template <int SRC>
 DEV void step_action(RegEnv &R, const uint8_t *act_in, size_t i, uint32_t &srng, uint8_t act[5]) {
-  if (SRC == MASK_SELECTED) sample_heads(R.sel, srng, act);
-  else if (SRC == MASK_STORED) sample_heads(R.sta, srng, act);
+  if (SRC == MASK_SELECTED) sample_heads(R.sel, srng, act, R.tab);
+  else if (SRC == MASK_STORED) sample_heads(R.sta, srng, act, R.tab);
   else {
     const uint8_t *ai = act_in + i * COG_ACTION_BYTES;
     const uint8_t top[5] = {COG_N_CARDTYPES, COG_N_CARDTYPES, COG_N_CARDTYPES, 6, COG_N_SHOP};
@@ -1853,7 +1887,8 @@ DEV bool end_of_step(const DevState &s, size_t i, bool was_done, bool finish, ui
 // One step of env i: load (two rounds; the sampler runs on round 1 while round 2 is in
 // flight), step on registers, store what changed, [finish / auto-reset].
 template <int SRC>
-DEV bool env_step_lane(const DevState &s, size_t i, const uint8_t *act_in, uint32_t *rngs, uint8_t *actions_out) {
+DEV bool env_step_lane(const DevState &s, size_t i, const uint8_t *act_in, uint32_t *rngs, uint8_t *actions_out,
+                       const UidEntry *tab) {
   STAMP(s, 0);
   PH_DECL;
   Snap S;
@@ -1861,6 +1896,7 @@ DEV bool env_step_lane(const DevState &s, size_t i, const uint8_t *act_in, uint3
   load_env(s, i, S);
   uint32_t srng = SRC == MASK_EXTERNAL ? 0u : rngs[i];
   regs_env(R, S);
+  R.tab = tab;
   const int ag = (int)R.agent();
   const int na = ag + 1 >= (int)R.n_players() ? 0 : ag + 1;
   load_players(s, i, ag, na, S);
@@ -1888,9 +1924,11 @@ DEV bool env_step_lane(const DevState &s, size_t i, const uint8_t *act_in, uint3
 template <int SRC>
 __global__ void __launch_bounds__(64) k_env_step(DevState s, const uint8_t *__restrict__ act_in, uint32_t *__restrict__ rngs,
                                                  uint8_t *__restrict__ actions_out) {
+  __shared__ UidEntry tab[kUidTab];
+  uid_tab_fill(tab);
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool enc = false;
-  if (i < s.n) enc = env_step_lane<SRC>(s, i, act_in, rngs, actions_out);
+  if (i < s.n) enc = env_step_lane<SRC>(s, i, act_in, rngs, actions_out, tab);
   wave_encode(s, i < s.n ? i : 0, enc);                    // converged: the whole wave encodes
   STAMP(s, 5);
 }
@@ -1906,6 +1944,7 @@ struct LaneLds {
   uint4 pl[4][NL];
   uint2 cells[4][NL];
   uint4 heads[4][NL];                 // stored masks (MBits + pad)
+  UidEntry tab[kUidTab];              // the uniform's division table
 };
 template <class LaneLds>
 DEV void lds_fill_players(LaneLds &L, const DevState &s, size_t i, int l) {
@@ -2002,6 +2041,7 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s, int steps, uint32_t
     if (live && t >= t_first) {
       RegEnv R;
       regs_env(R, S);
+      R.tab = L.tab;
       const int ag = (int)R.agent();                       // S holds ag's and na's records: read
       const int na = ag + 1 >= (int)R.n_players() ? 0 : ag + 1;   // at the end of the last step
       uint8_t act[5];
@@ -2011,7 +2051,7 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s, int steps, uint32_t
       {                                                    // sampler's cost, measured by running
         uint32_t r2 = srng ^ 0x5555u;                      // it a second time on a discarded state
         uint8_t a2[5];
-        sample_heads(R.sel, r2, a2);
+        sample_heads(R.sel, r2, a2, R.tab);
         asm volatile("" ::"v"((uint32_t)a2[0] | a2[1] << 8 | a2[2] << 16 | (uint32_t)a2[3] << 24), "v"(a2[4] ^ r2));
       }
 #endif
@@ -2022,12 +2062,24 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s, int steps, uint32_t
       const bool finish = !was_done && step_regs(R, act, s, i, na PH_PASS);
       if (finish) R.set_done(1u);
       PH(2);
+      // the player records to this wave's LDS, and the next step's players back, before the
+      // store phase: the LDS round trip overlaps the stores instead of stalling the loop's tail
+      L.pl[ag][l] = pack_player(R.P);
+      L.cells[ag][l] = R.cells_a;
+      L.heads[ag][l] = mbits_u4(bits_of(R.sta));
+      if (na != ag) L.heads[na][l] = mbits_u4(bits_of(R.stn));
+#pragma unroll
+      for (int k = 0; k < 7; k++) L.deck[ag][k][l] = make_uint4(R.d[4 * k], R.d[4 * k + 1], R.d[4 * k + 2], R.d[4 * k + 3]);
+      uint32_t agent = R.agent();
+      Snap N;                                              // the next step's player records
+      lds_players(L, l, (int)agent, next_of((int)agent), N);
+      PH(3);
 #ifndef COG_ABLATE_STORES                                  // diagnostic timing builds only
       store_outputs(s, i, ag, na, S, R);
       store_action(actions_out + i * COG_ACTION_BYTES, act);
 #endif
-      PH(3);
-      // the next step's image: registers (env level) and this wave's LDS (player level)
+      PH(4);
+      // the next step's image: registers (env level) and the player records just read
       S.g0 = make_uint4(R.rng, R.seed, R.max_steps, R.turn_counter);
       S.g1 = make_uint4(R.g1x, R.g1y, R.in_market, R.flags);
       S.g2 = R.g2;
@@ -2036,14 +2088,9 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s, int steps, uint32_t
 #pragma unroll
       for (int k = 0; k < 3; k++) S.sh[k] = make_uint4(R.sh[4 * k], R.sh[4 * k + 1], R.sh[4 * k + 2], R.sh[4 * k + 3]);
       S.sel = bits_of(R.sel);
-      L.pl[ag][l] = pack_player(R.P);
-      L.cells[ag][l] = R.cells_a;
-      L.heads[ag][l] = mbits_u4(bits_of(R.sta));
-      if (na != ag) L.heads[na][l] = mbits_u4(bits_of(R.stn));
+      S.pla = N.pla; S.pln = N.pln; S.ca = N.ca; S.cn = N.cn; S.sta = N.sta; S.stn = N.stn;
 #pragma unroll
-      for (int k = 0; k < 7; k++) L.deck[ag][k][l] = make_uint4(R.d[4 * k], R.d[4 * k + 1], R.d[4 * k + 2], R.d[4 * k + 3]);
-      PH(4);
-      uint32_t agent = R.agent();
+      for (int k = 0; k < 7; k++) S.dk[k] = N.dk[k];
       if (was_done || finish) {                            // episode end: state to HBM first
         store_private_all(s, i, S, L, l);
         if (!FIX) {                                        // hand the env to the fix-up pass
@@ -2056,11 +2103,10 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s, int steps, uint32_t
         load_env(s, i, S);                                 // reset: reload from the stored state
         lds_fill_players(L, s, i, l);
         agent = S.g1.y & 0xffu;
+        lds_players(L, l, (int)agent, next_of((int)agent), S);
       } else {
         enc = end_of_step(s, i, false, false, agent, out);
       }
-      lds_players(L, l, (int)agent, next_of((int)agent), S);   // the next step's players, early:
-                                                           // the reads overlap the loop's tail
       PH(5);
     }
     if (FIX) wave_encode(s, i, enc);                       // converged: the whole wave encodes
@@ -2078,6 +2124,7 @@ template <int SRC, int NL>
 __global__ void __launch_bounds__(NL) k_env_rollout(DevState s, int steps, uint32_t *__restrict__ rngs,
                                                     uint8_t *__restrict__ actions_out) {
   __shared__ LaneLds<NL> L;
+  uid_tab_fill(L.tab);
   const uint32_t park = rollout_pass<SRC, false, NL>(L, s, steps, rngs, actions_out, kParkNone);
   if (__builtin_amdgcn_ballot_w64(park != kParkNone))    // (wave-uniform)
     rollout_pass<SRC, true, NL>(L, s, steps, rngs, actions_out, park);
@@ -2086,11 +2133,13 @@ __global__ void __launch_bounds__(NL) k_env_rollout(DevState s, int steps, uint3
 
 __global__ void __launch_bounds__(256) k_sample(size_t n, const uint8_t *__restrict__ masks,
                                                 uint32_t *__restrict__ rngs, uint8_t *__restrict__ actions) {
+  __shared__ UidEntry tab[kUidTab];
+  uid_tab_fill(tab);
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t rng = rngs[i];
   uint8_t a[5];
-  sample_mask(masks + i * COG_MASK_BYTES, rng, a);
+  sample_mask(masks + i * COG_MASK_BYTES, rng, a, tab);
   rngs[i] = rng;
   store_action(actions + i * COG_ACTION_BYTES, a);
 }

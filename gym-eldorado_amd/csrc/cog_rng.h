@@ -101,6 +101,22 @@ COG_HD uint32_t uid_small(uint32_t &x, uint32_t k) {       // k in [1, 31]
 // every draw a k in [1, 31] can reject has r >= range - 30 (range mod k <= 30)
 constexpr uint32_t kSmallSafe = kUrngRange - 31u;
 
+// Table form for k in [1, 31] (the kernels keep the table in LDS): entry k = {s, m} with
+// s = range / k and m = floor(2^32 / s).  For an accepted r (< k s < 2^31) the quotient r / s is
+// q' = mulhi(r, m) or q' + 1: r m / 2^32 > r / s - r / 2^32 > r / s - 1/2, so q' >= r / s - 1;
+// and r - q' s < 2 s < 2^32, so the correction is one exact 32-bit compare.
+struct UidEntry {
+  uint32_t s, m;
+};
+constexpr UidEntry uid_entry(uint32_t k) {
+  return k == 0 ? UidEntry{1u, 0u} : UidEntry{kUrngRange / k, (uint32_t)((1ull << 32) / (kUrngRange / k))};
+}
+constexpr int kUidTab = 32;                                // k = 0 .. 31
+COG_HD uint32_t uid_tab_accepted(uint32_t r, uint32_t s, uint32_t m) {
+  const uint32_t q = (uint32_t)(((uint64_t)r * m) >> 32);
+  return q + (r - q * s >= s ? 1u : 0u);
+}
+
 // Jump-ahead: the state j steps on is x * 16807^j mod (2^31 - 1), so the states of several
 // consecutive draws are independent products instead of a serial chain.
 constexpr uint32_t kMinstdM = 0x7fffffffu;

@@ -25,6 +25,16 @@ extern "C" void run(const uint32_t *x0, const uint32_t *k, uint32_t n, int which
     xout[i] = x;
   }
 }
+// the table form: one accepted draw, r < k s (uid_small_accepted's precondition as well)
+extern "C" uint32_t run_tab(const uint32_t *r, const uint32_t *k, uint32_t n, uint32_t *out) {
+  uint32_t bad = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const cog::UidEntry e = cog::uid_entry(k[i]);
+    out[i] = cog::uid_tab_accepted(r[i], e.s, e.m);
+    bad += out[i] != cog::uid_small_accepted(r[i], k[i]);
+  }
+  return bad;
+}
 // mr_jump(x, 16807^j) for j = 1..4 against j sequential mr_next steps
 extern "C" uint32_t run_jump(const uint32_t *x0, uint32_t n) {
   uint32_t bad = 0;
@@ -51,6 +61,8 @@ def lib(tmp_path_factory):
     lib.run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
     lib.run_jump.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
     lib.run_jump.restype = ctypes.c_uint32
+    lib.run_tab.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+    lib.run_tab.restype = ctypes.c_uint32
     return lib
 
 
@@ -108,3 +120,25 @@ def test_jump_ahead(lib):
     x0 = np.concatenate([np.array([1, 2, 16807, P - 2, P - 1, 2 ** 30, 2 ** 31 - 2], dtype=np.uint64),
                          rng.integers(1, P, size=1_000_000, dtype=np.uint64)]).astype(np.uint32)
     assert lib.run_jump(x0.ctypes.data, len(x0)) == 0
+
+
+def test_table_uniform(lib):
+    """uid_tab_accepted (the LDS-table form the kernels use for k <= 31) equals r / (range / k) on
+    every quotient boundary of every k and on random accepted draws."""
+    rs, ks = [], []
+    for k in range(1, 32):
+        s = RANGE // k
+        for j in range(1, k + 1):
+            rs += [j * s - 2, j * s - 1, j * s, j * s + 1]
+        rs += [0, 1, k * s - 1]
+        ks += [k] * (4 * k + 3)
+    rng = np.random.default_rng(5)
+    kr = rng.integers(1, 32, size=1_000_000)
+    rr = (rng.random(kr.size) * (RANGE // kr * kr)).astype(np.int64)
+    r = np.concatenate([np.array(rs, dtype=np.int64), rr])
+    k = np.concatenate([np.array(ks, dtype=np.int64), kr])
+    keep = (r >= 0) & (r < (RANGE // k) * k)
+    r, k = r[keep].astype(np.uint32), k[keep].astype(np.uint32)
+    out = np.empty_like(r)
+    assert lib.run_tab(r.ctypes.data, k.ctypes.data, len(r), out.ctypes.data) == 0
+    assert np.array_equal(out, (r.astype(np.int64) // (RANGE // k.astype(np.int64))).astype(np.uint32))
