@@ -1959,6 +1959,42 @@ DEV void lds_fill_players(LaneLds &L, const DevState &s, size_t i, int l) {
     L.heads[p][l] = s.heads[5 * i + 1 + p];
   }
 }
+// The wave's player records are stored cooperatively at the end of a launch: consecutive
+// work-items take consecutive 16-B granules of one env's records (its counters and neighbourhood
+// caches are EnvPriv granules 4..9, its stored-mask bit vectors 4 consecutive heads), so one
+// store instruction covers a few contiguous runs instead of 64 envs' scattered granules.
+// Measured (tools/fixedcost.sh): the per-work-item store cost 6.2 us per launch at 65,536 envs,
+// this one about 1 us.  The same transposition for the launch's loads was slower (19.7 against
+// 9.5 us): those stay one env per work-item (lds_fill_players).  ne = the wave's envs; a
+// work-item past the end of a ragged last wave stores env ne - 1's records again.
+template <class LaneLds, int NL>
+DEV void lds_store_wave(const LaneLds &L, const DevState &s, size_t base, int ne) {
+  const int l = threadIdx.x;                               // (past the end: env ne - 1's records again)
+#pragma unroll
+  for (int j = 0; j < 4 * NL / 64; j++) {
+    const int f = j * 64 + l, e = min(f >> 2, ne - 1), q = f & 3;
+    reinterpret_cast<uint4 *>(s.priv + base + e)[4 + q] = L.pl[q][e];
+  }
+#pragma unroll
+  for (int j = 0; j < 2 * NL / 64; j++) {
+    const int f = j * 64 + l, e = min(f >> 1, ne - 1), q = f & 1;
+    const uint2 a = L.cells[2 * q][e], b = L.cells[2 * q + 1][e];
+    reinterpret_cast<uint4 *>(s.priv + base + e)[8 + q] = make_uint4(a.x, a.y, b.x, b.y);
+  }
+#pragma unroll
+  for (int j = 0; j < 4 * NL / 64; j++) {
+    const int f = j * 64 + l, e = min(f >> 2, ne - 1), p = f & 3;
+    s.heads[5 * (base + e) + 1 + p] = L.heads[p][e];
+  }
+}
+// the env-level private records of env i (EnvPriv granules 0, 1, 3, the selected mask's bits)
+DEV void store_env_private(const DevState &s, size_t i, const Snap &S) {
+  uint4 *pw = reinterpret_cast<uint4 *>(s.priv + i);
+  pw[0] = S.g0;
+  pw[1] = S.g1;
+  reinterpret_cast<uint32_t *>(pw + 3)[0] = S.info_steps;
+  s.heads[5 * i] = mbits_u4(S.sel);
+}
 // every private record of env i (EnvPriv granules 0, 1, 3, all players, all mask bit vectors)
 // from the rollout's on-chip copies
 template <class LaneLds>
@@ -2011,9 +2047,12 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s, int steps, uint32_t
   auto next_of = [&](int a) { return a + 1 >= (int)(S.g1.x & 0xffu) ? 0 : a + 1; };   // n_players
   if (live) {
     load_env(s, i, S);
+#ifndef COG_ABLATE_FILL                                    // diagnostic timing builds only
     lds_fill_players(L, s, i, l);
+#endif
     srng = rngs[i];
   }
+
   if (FIX) {                                               // step `park`'s episode end
     bool enc = false;
     if (live) {
@@ -2112,8 +2151,8 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s, int steps, uint32_t
     if (FIX) wave_encode(s, i, enc);                       // converged: the whole wave encodes
     PH(6);
   }
-  if (live) {                                              // private state back to HBM
-    store_private_all(s, i, S, L, l);
+  if (live) {                                              // env-level private state back to HBM
+    store_env_private(s, i, S);                            // (the player records: lds_store_wave)
     rngs[i] = srng;
   }
   if (!FIX) PH_FLUSH(s);
@@ -2124,10 +2163,16 @@ template <int SRC, int NL>
 __global__ void __launch_bounds__(NL) k_env_rollout(DevState s, int steps, uint32_t *__restrict__ rngs,
                                                     uint8_t *__restrict__ actions_out) {
   __shared__ LaneLds<NL> L;
+  const size_t base = (size_t)blockIdx.x * NL;
+  const int ne = (int)min((size_t)NL, s.n - base);
   uid_tab_fill(L.tab);
   const uint32_t park = rollout_pass<SRC, false, NL>(L, s, steps, rngs, actions_out, kParkNone);
   if (__builtin_amdgcn_ballot_w64(park != kParkNone))    // (wave-uniform)
     rollout_pass<SRC, true, NL>(L, s, steps, rngs, actions_out, park);
+  __syncthreads();
+#ifndef COG_ABLATE_EPI                                     // diagnostic timing builds only
+  lds_store_wave<LaneLds<NL>, NL>(L, s, base, ne);
+#endif
 }
 
 
@@ -2214,9 +2259,9 @@ static void rollout_launch(const DevState &s, int mask_source, int steps, uint32
 }
 int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions, void *stream) {
   if (!s.n || steps <= 0) return 0;
-  // one 64-env wave per workgroup: 32-env workgroups (two waves per SIMD at 65,536 envs) measured
-  // 7.3 us/step against 3.8 (tools/lanes_ab.sh, round 2): the SIMD already issues one of this
-  // integer code's instructions per quad-cycle with a single wave
+  // one 64-env wave per workgroup: 32-env workgroups measured 7.3 us/step against 3.8 at 65,536
+  // envs (round 2).  The kernel's register allocation (about 490 VGPRs + AGPRs per work-item)
+  // admits one wave per SIMD, so 2,048 half-empty waves ran in two rounds on 1,024 SIMDs
   rollout_launch<64>(s, mask_source, steps, d_rng, d_actions, (hipStream_t)stream);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

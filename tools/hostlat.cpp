@@ -68,5 +68,23 @@ int main(int argc, char **argv) {
   printf("n=%zu K=%d: wall(rollout+sync) %.1f us, device(events) %.1f us, wall(rollout+streamsync) %.1f us, "
          "idle streamsync %.1f us, idle runner sync %.1f us\n",
          n, K, median(wall), median(dev), median(wall2), median(ssync), median(rsync));
+  // device time of one launch against its step count: the intercept is the fixed per-launch cost
+  for (int k : {1, 2, 5, 20, 100}) {
+    std::vector<double> d, w;
+    cog_runner_set_chunk(run, k);
+    for (int r = 0; r < 20; r++) {
+      double ms;
+      uint64_t kk;
+      cog_runner_set_timing(run, 1);
+      const double t0 = now_us();
+      cog_runner_rollout(run, k);
+      cog_runner_sync(run);
+      w.push_back(now_us() - t0);
+      cog_runner_kernel_time(run, &ms, &kk);
+      cog_runner_set_timing(run, 0);
+      d.push_back(ms * 1e3);
+    }
+    printf("  K=%4d  device %.1f us  wall %.1f us\n", k, median(d), median(w));
+  }
   return 0;
 }
