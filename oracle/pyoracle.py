@@ -137,6 +137,10 @@ class _Lib:
             lib.ref_sample.argtypes = [vp, vp]
             lib.ref_sampler_actions.restype = vp
             lib.ref_sampler_actions.argtypes = [vp]
+            lib.ref_layout_name.restype = C.c_char_p
+            lib.ref_layout_name.argtypes = [C.c_int]
+            lib.ref_layout_offset.restype = C.c_size_t
+            lib.ref_layout_offset.argtypes = [C.c_int]
             cls._ref = lib
         return cls._ref
 
@@ -212,6 +216,16 @@ class OracleSampler:
             self.lib.orc_sampler_destroy(self.h)
         except Exception:
             pass
+
+
+def ref_layout():
+    """{"ObsData.player_data[0].action_mask.play": offset, ...} from the reference build."""
+    L = _Lib.ref()
+    return {L.ref_layout_name(k).decode(): int(L.ref_layout_offset(k)) for k in range(L.ref_layout_count())}
+
+
+def ref_available():
+    return os.path.exists(REF_SO)
 
 
 def run_threaded(vec: OracleVec, sampler: OracleSampler, steps: int, n_threads: int) -> float:

@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <vector>
 
 using env1 = vec_cog_env<1>;
 using smp1 = vec_action_sampler<1>;
@@ -72,6 +73,42 @@ size_t ref_sizeof(int which) {
   default: return 0;
   }
 }
+// Field offsets of the reference's records (api.h:67-161), by dotted numpy field path, so the
+// layout test pins every named field against the reference build rather than a restatement.
+// (Address differences inside one object: offsetof cannot index a std::array.)
+struct RefField {
+  const char *name;
+  size_t off;
+};
+static std::vector<RefField> ref_layout() {
+  static ObsData o;
+  static ActionMask m;
+  static ActionData a;
+  static Info f;
+#define D(obj, T, path) RefField{#T "." #path, (size_t)((const char *)&obj.path - (const char *)&obj)}
+  return {
+      D(o, ObsData, shared), D(o, ObsData, shared.map), D(o, ObsData, shared.phase),
+      D(o, ObsData, shared.current_resources), D(o, ObsData, shared.shop), D(o, ObsData, player_data),
+      D(o, ObsData, player_data[1]), D(o, ObsData, player_data[3]), D(o, ObsData, player_data[0].obs.draw),
+      D(o, ObsData, player_data[0].obs.hand), D(o, ObsData, player_data[0].obs.active),
+      D(o, ObsData, player_data[0].obs.played), D(o, ObsData, player_data[0].obs.discard),
+      D(o, ObsData, player_data[0].action_mask), D(o, ObsData, player_data[0].action_mask.play),
+      D(o, ObsData, player_data[0].action_mask.play_special), D(o, ObsData, player_data[0].action_mask.remove),
+      D(o, ObsData, player_data[0].action_mask.move), D(o, ObsData, player_data[0].action_mask.get_from_shop),
+      D(m, ActionMask, play), D(m, ActionMask, play_special), D(m, ActionMask, remove), D(m, ActionMask, move),
+      D(m, ActionMask, get_from_shop), D(a, ActionData, play), D(a, ActionData, play_special),
+      D(a, ActionData, remove), D(a, ActionData, move), D(a, ActionData, get_from_shop), D(f, Info, total_length),
+      D(f, Info, agent_infos), D(f, Info, agent_infos[1]), D(f, Info, agent_infos[0].steps_taken),
+      D(f, Info, agent_infos[0].returns), D(f, Info, agent_infos[0].travelled_hexes),
+      D(f, Info, agent_infos[0].cards_added), D(f, Info, agent_infos[0].cards_removed),
+      D(f, Info, agent_infos[0].n_machete_uses), D(f, Info, agent_infos[0].n_paddle_uses),
+      D(f, Info, agent_infos[0].n_coin_uses), D(f, Info, agent_infos[0].n_card_uses),
+  };
+#undef D
+}
+int ref_layout_count() { return (int)ref_layout().size(); }
+const char *ref_layout_name(int k) { return ref_layout()[k].name; }
+size_t ref_layout_offset(int k) { return ref_layout()[k].off; }
 void *ref_sampler_create(uint32_t seed) { return new smp1(seed); }
 void ref_sampler_destroy(void *s) { delete static_cast<smp1 *>(s); }
 void ref_sample(void *s, const void *mask) {

@@ -61,6 +61,32 @@ def test_dtypes_match_reference_layout(cg):
     assert cg.ObsData.dtype["player_data"].base["action_mask"]["play"] == np.dtype(("?", (22,)))
 
 
+def dtype_offset(dt, path):
+    """Byte offset of a dotted numpy field path ("player_data[1].obs.hand") in dtype dt."""
+    off = 0
+    for part in path.split("."):
+        m = re.fullmatch(r"(\w+)(?:\[(\d+)\])?", part)
+        sub, o = dt.fields[m.group(1)][:2]
+        off += o
+        if m.group(2) is not None:
+            off += int(m.group(2)) * sub.base.itemsize
+            sub = sub.base
+        dt = sub
+    return off
+
+
+def test_field_offsets_match_the_reference_build(cg):
+    """Every named field's offset in the module's dtypes against offsetof-style addresses taken
+    in a build of the unmodified reference headers (oracle/ref_harness.cpp, oracle/_ref)."""
+    if not po.ref_available():
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    lay = po.ref_layout()
+    assert len(lay) >= 40
+    for name, ref_off in lay.items():
+        rec, path = name.split(".", 1)
+        assert dtype_offset(np.dtype(getattr(cg, rec)), path) == ref_off, name
+
+
 def test_no_gpu_fails_loudly(cg):
     if cg.device_count() > 0:
         pytest.skip("a GPU is present")
