@@ -379,10 +379,14 @@ def main():
         runner.set_chunk(chunk)
         enc_ms = env.time_encode(20)
         enc_gbs = ENCODE_BYTES * n / (enc_ms / 1e3) / 1e9
-        cp = copy_peak_gbs(d)
+        cp_torch = copy_peak_gbs(d)
+        cp = cg._city_of_gold.time_copy(dev, 1 << 31, 5)
         extras["encode"] = {"kernel": "k_encode", "ms": enc_ms, "achieved": enc_gbs, "unit": "GB/s",
                             "frac": enc_gbs / HBM_PEAK_GBS, "copy_peak_GBs": cp,
                             "frac_of_copy_peak": enc_gbs / cp if cp else None,
+                            "copy_peak_note": "the engine's copy kernel (16-B loads/stores, plain or non-temporal, 8 or 32 waves per CU: the fastest), "
+                                              "2 x 2 GiB buffers, read + write bytes); torch's copy_ in the "
+                                              "same run: %.0f GB/s" % cp_torch if cp_torch else "",
                             "algorithmic_bytes_per_launch": ENCODE_BYTES * n}
         del runner, smp, env
         # full dynamics: stored masks (moves, shop, specials), episodes of 30 turns -> auto-resets

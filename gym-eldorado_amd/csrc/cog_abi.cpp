@@ -9,14 +9,20 @@
 // slice.  Every operation is issued on all shards' streams first and waited for afterwards, so
 // the GPUs of a handle run concurrently.
 //
-// Device layout per shard (one allocation `outs`, so a host-visible step needs two D2H copies:
-// this block and the strided ObsData tail):
+// Device layout per shard (one allocation `outs`, padded to 16 B):
 //   [status 64 B][selected masks n x 128][infos n x 192][rewards n x 16][dones n][agents n]
+// Host views are pinned, device-mapped, coherent memory.  A host-visible call ends with one
+// publish kernel per shard (cog_engine.hip k_publish): the ObsData tails and this block are
+// compared with an HBM copy of what the host views hold, and the granules that changed are
+// stored straight into the views -- no D2H copy commands.  Actions and masks the caller passes
+// in the engine's own pinned views are read by the kernels in place (zero-copy); other host
+// arrays are staged by an H2D copy.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <random>
 #include <string>
 #include <vector>
@@ -79,6 +85,57 @@ int hmalloc(T **p, size_t bytes, unsigned flags = hipHostMallocDefault) {
   return COG_OK;
 }
 
+// Pinned, device-mapped, coherent host memory (uncached on the GPU: kernels read what the host
+// last wrote).  Registered so that a caller's pointer into one of these views can be handed to a
+// kernel without a staging copy.
+constexpr unsigned kZcFlags = hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable;
+struct ZcRange {
+  const uint8_t *base;
+  size_t bytes;
+  const uint8_t *dev;                 // the device address of base
+};
+std::mutex g_zc_mu;
+std::vector<ZcRange> g_zc;
+
+template <class T>
+int zc_alloc(T **p, size_t bytes) {
+  int rc = hmalloc(p, bytes, kZcFlags);
+  if (rc) return rc;
+  void *d = nullptr;
+  if (hipHostGetDevicePointer(&d, *p, 0) != hipSuccess) d = nullptr;
+  std::lock_guard<std::mutex> lk(g_zc_mu);
+  g_zc.push_back({reinterpret_cast<const uint8_t *>(*p), bytes ? bytes : 64, static_cast<const uint8_t *>(d)});
+  return COG_OK;
+}
+void zc_free(void *p) {
+  if (!p) return;
+  {
+    std::lock_guard<std::mutex> lk(g_zc_mu);
+    for (size_t j = 0; j < g_zc.size(); j++)
+      if (g_zc[j].base == p) {
+        g_zc.erase(g_zc.begin() + (long)j);
+        break;
+      }
+  }
+  (void)hipHostFree(p);
+}
+// the device address of [p, p + bytes) when the range lies inside one of the engine's mapped
+// views, else nullptr (the caller stages a copy)
+const uint8_t *zc_device(const void *p, size_t bytes) {
+  const uint8_t *q = static_cast<const uint8_t *>(p);
+  std::lock_guard<std::mutex> lk(g_zc_mu);
+  for (const ZcRange &r : g_zc)
+    if (r.dev && q >= r.base && q + bytes <= r.base + r.bytes) return r.dev + (q - r.base);
+  return nullptr;
+}
+// every device of a multi-GPU handle must see a view at the address recorded at allocation
+bool zc_same_on(int device, const void *p) {
+  DeviceGuard g(device);
+  void *d = nullptr;
+  if (hipHostGetDevicePointer(&d, const_cast<void *>(p), 0) != hipSuccess) return false;
+  return d == zc_device(p, 1);
+}
+
 // the reference runner's block split (runner.h:33-38): n / k per block, the last takes the rest
 std::vector<size_t> block_split(size_t n, int k) {
   std::vector<size_t> first(k + 1);
@@ -90,7 +147,7 @@ std::vector<size_t> block_split(size_t n, int k) {
 
 constexpr size_t kStatusBytes = 64;
 struct OutLayout {                    // offsets inside a shard's `outs` block (device and host)
-  size_t sel, info, rew, done, agent, total;
+  size_t sel, info, rew, done, agent, total, alloc;
   explicit OutLayout(size_t n) {
     sel = kStatusBytes;
     info = sel + n * COG_MASK_BYTES;
@@ -98,6 +155,7 @@ struct OutLayout {                    // offsets inside a shard's `outs` block (
     done = rew + n * 4 * sizeof(float);
     agent = done + n;
     total = agent + n;
+    alloc = (total + 15) & ~(size_t)15;   // whole granules: the publish kernel moves 16 B at a time
   }
 };
 
@@ -113,6 +171,11 @@ struct EnvShard {
   uint8_t *h_outs = nullptr;          // pinned host mirror of `outs`
   uint8_t *d_actions = nullptr;       // staging for host-provided actions
   bool status_dirty = false;          // device status words may be non-zero
+  // publish path (host views): the device addresses of this shard's slice of the views, and
+  // `mir`, an HBM copy of what they hold (valid once a publish stored every granule)
+  bool zc = false;
+  uint8_t *h_obs_d = nullptr, *h_outs_d = nullptr, *mir = nullptr;
+  bool mir_valid = false;
 };
 
 struct cog_env {
@@ -168,20 +231,18 @@ void env_free(cog_env *e) {
   for (EnvShard &k : e->sh) {
     DeviceGuard g(k.device);
     if (k.stream) (void)hipStreamSynchronize(k.stream);
-    void *dev[] = {k.s.obs, k.outs, k.s.priv, k.s.grid, k.s.cgrid, k.s.heads, k.s.gen, k.s.dirty, k.d_actions};
+    void *dev[] = {k.s.obs, k.outs, k.s.priv, k.s.grid, k.s.cgrid, k.s.heads, k.s.gen, k.s.dirty, k.d_actions, k.mir};
     for (void *p : dev)
       if (p) (void)hipFree(p);
-    if (k.h_outs) (void)hipHostFree(k.h_outs);
+    zc_free(k.h_outs);
     if (k.ev) (void)hipEventDestroy(k.ev);
     if (k.stream) (void)hipStreamDestroy(k.stream);
   }
-  void *hst[] = {e->h_obs, e->h_err};
-  for (void *p : hst)
-    if (p) (void)hipHostFree(p);
+  zc_free(e->h_obs);
+  if (e->h_err) (void)hipHostFree(e->h_err);
   if (!single(e)) {
     void *more[] = {e->h_sel, e->h_rew, e->h_done, e->h_agent, e->h_info};
-    for (void *p : more)
-      if (p) (void)hipHostFree(p);
+    for (void *p : more) zc_free(p);
   }
   delete e;
 }
@@ -236,11 +297,36 @@ void gather_small(cog_env *e) {
 // from the host-mapped error words after the stream sync, with no copy; host-visible work reads
 // the status words that came with its refresh copy.  Regenerated maps (auto-resets) are copied
 // to the host views afterwards.  Status words are cleared only when they are non-zero.
-int finish(cog_env *e, bool refresh_host) {
+int enqueue_publish(EnvShard &k, const SamplerShard *q, uint8_t *h_act_d) {
+  if (!k.n) return COG_OK;
+  const OutLayout L(k.n);
+  if (cog::launch_publish(k.s, k.outs, k.mir, k.h_obs_d, k.h_outs_d, L.alloc, k.mir_valid ? 0 : 1,
+                          q ? q->d_actions : nullptr, q ? h_act_d : nullptr, k.stream))
+    return fail(COG_ERR_HIP, std::string("publish launch failed: ") + hipGetErrorString(hipGetLastError()));
+  k.mir_valid = true;
+  return COG_OK;
+}
+
+// smp (optional): a runner's sampler whose actions' host view is refreshed with the env's
+int finish(cog_env *e, bool refresh_host, cog_sampler *smp = nullptr) {
   const bool host = refresh_host && e->host;
-  for (EnvShard &k : e->sh) {
+  for (size_t j = 0; j < e->sh.size(); j++) {
+    EnvShard &k = e->sh[j];
     DeviceGuard g(k.device);
-    int rc = host ? enqueue_refresh(e, k) : COG_OK;
+    int rc = COG_OK;
+    if (host && k.zc) {
+      const SamplerShard *q = smp ? &smp->sh[j] : nullptr;
+      uint8_t *h_act = q ? const_cast<uint8_t *>(zc_device(smp->h_actions + q->first, q->n * COG_ACTION_BYTES)) : nullptr;
+      if (q && q->n && !h_act)
+        HIPCHK(hipMemcpyAsync(smp->h_actions + q->first, q->d_actions, q->n * COG_ACTION_BYTES, hipMemcpyDeviceToHost,
+                              k.stream));
+      rc = enqueue_publish(k, h_act ? q : nullptr, h_act);
+    } else if (host) {
+      if (smp && smp->sh[j].n)
+        HIPCHK(hipMemcpyAsync(smp->h_actions + smp->sh[j].first, smp->sh[j].d_actions,
+                              smp->sh[j].n * COG_ACTION_BYTES, hipMemcpyDeviceToHost, k.stream));
+      rc = enqueue_refresh(e, k);
+    }
     if (rc) return rc;
   }
   int rc = sync_all(e);
@@ -312,6 +398,7 @@ int refresh_full(cog_env *e) {
   }
   int rc = sync_all(e);
   if (rc) return rc;
+  for (EnvShard &k : e->sh) k.mir_valid = false;   // the views now hold what no mirror recorded
   gather_small(e);
   return COG_OK;
 }
@@ -333,7 +420,7 @@ void sampler_free(cog_sampler *s) {
       if (p) (void)hipFree(p);
     if (k.stream) (void)hipStreamDestroy(k.stream);
   }
-  if (s->h_actions) (void)hipHostFree(s->h_actions);
+  zc_free(s->h_actions);
   delete s;
 }
 
@@ -354,13 +441,13 @@ int env_shard_init(EnvShard &k, uint32_t default_seed, uint32_t *err_word) {
   const OutLayout L(n);
   cog::DevState &s = k.s;
   int rc;
-  if ((rc = dmalloc(&s.obs, n * COG_OBS_BYTES)) || (rc = dmalloc(&k.outs, L.total)) ||
+  if ((rc = dmalloc(&s.obs, n * COG_OBS_BYTES)) || (rc = dmalloc(&k.outs, L.alloc)) ||
       (rc = dmalloc(&s.priv, n * sizeof(cog::EnvPriv))) || (rc = dmalloc(&s.grid, n * (size_t)cog::kGridBytes)) ||
       (rc = dmalloc(&s.cgrid, n * (size_t)COG_CELLS)) || (rc = dmalloc(&s.heads, n * 5 * sizeof(uint4))) ||
       (rc = dmalloc(&s.gen, n * sizeof(cog::GenScratch))) || (rc = dmalloc(&s.dirty, n * sizeof(uint32_t))) ||
-      (rc = dmalloc(&k.d_actions, n * COG_ACTION_BYTES)) || (rc = hmalloc(&k.h_outs, L.total)))
+      (rc = dmalloc(&k.d_actions, n * COG_ACTION_BYTES)) || (rc = zc_alloc(&k.h_outs, L.alloc)))
     return rc;
-  std::memset(k.h_outs, 0, L.total);
+  std::memset(k.h_outs, 0, L.alloc);
   s.n = n;
   s.first = k.first;
   s.cap = n;
@@ -374,7 +461,7 @@ int env_shard_init(EnvShard &k, uint32_t default_seed, uint32_t *err_word) {
   void *d_err = nullptr;
   HIPCHK(hipHostGetDevicePointer(&d_err, err_word, 0));
   s.err = static_cast<uint32_t *>(d_err);
-  struct { void *p; size_t b; } z[] = {{s.obs, n * COG_OBS_BYTES}, {k.outs, L.total}, {s.grid, n * (size_t)cog::kGridBytes},
+  struct { void *p; size_t b; } z[] = {{s.obs, n * COG_OBS_BYTES}, {k.outs, L.alloc}, {s.grid, n * (size_t)cog::kGridBytes},
                                        {s.cgrid, n * (size_t)COG_CELLS}, {s.gen, n * sizeof(cog::GenScratch)},
                                        {k.d_actions, n * COG_ACTION_BYTES}};
   for (auto &zz : z)
@@ -536,8 +623,12 @@ int cog_env_step(cog_env *env, const cog_action_t *actions, size_t n) {
   for (EnvShard &k : env->sh) {
     if (!k.n) continue;
     DeviceGuard g(k.device);
-    HIPCHK(hipMemcpyAsync(k.d_actions, actions + k.first, k.n * COG_ACTION_BYTES, hipMemcpyHostToDevice, k.stream));
-    if (cog::launch_step(launch_state(k, env->host), k.d_actions, k.stream))
+    const uint8_t *da = zc_device(actions + k.first, k.n * COG_ACTION_BYTES);   // read in place when pinned
+    if (!da) {
+      HIPCHK(hipMemcpyAsync(k.d_actions, actions + k.first, k.n * COG_ACTION_BYTES, hipMemcpyHostToDevice, k.stream));
+      da = k.d_actions;
+    }
+    if (cog::launch_step(launch_state(k, env->host), da, k.stream))
       return fail(COG_ERR_HIP, std::string("step launch failed: ") + hipGetErrorString(hipGetLastError()));
   }
   return finish(env, true);
@@ -546,7 +637,7 @@ int cog_env_step(cog_env *env, const cog_action_t *actions, size_t n) {
 static int alloc_host_views(cog_env *env) {
   const size_t n = env->n;
   int rc;
-  if ((rc = hmalloc(&env->h_obs, n * COG_OBS_BYTES))) return rc;
+  if ((rc = zc_alloc(&env->h_obs, n * COG_OBS_BYTES))) return rc;
   std::memset(env->h_obs, 0, n * COG_OBS_BYTES);   // padding bytes stay defined
   if (single(env)) {                                // views point straight into the copy target
     EnvShard &k = env->sh[0];
@@ -556,10 +647,21 @@ static int alloc_host_views(cog_env *env) {
     env->h_rew = reinterpret_cast<float *>(k.h_outs + L.rew);
     env->h_done = k.h_outs + L.done;
     env->h_agent = k.h_outs + L.agent;
-  } else if ((rc = hmalloc(&env->h_sel, n * COG_MASK_BYTES)) || (rc = hmalloc(&env->h_rew, n * 4 * sizeof(float))) ||
-             (rc = hmalloc(&env->h_done, n)) || (rc = hmalloc(&env->h_agent, n)) ||
-             (rc = hmalloc(&env->h_info, n * COG_INFO_BYTES))) {
+  } else if ((rc = zc_alloc(&env->h_sel, n * COG_MASK_BYTES)) || (rc = zc_alloc(&env->h_rew, n * 4 * sizeof(float))) ||
+             (rc = zc_alloc(&env->h_done, n)) || (rc = zc_alloc(&env->h_agent, n)) ||
+             (rc = zc_alloc(&env->h_info, n * COG_INFO_BYTES))) {
     return rc;
+  }
+  for (EnvShard &k : env->sh) {                     // the publish path, where every device maps the views
+    if (!k.n) continue;
+    const OutLayout L(k.n);
+    k.h_obs_d = const_cast<uint8_t *>(zc_device(env->h_obs + k.first, k.n * COG_OBS_BYTES));
+    k.h_outs_d = const_cast<uint8_t *>(zc_device(k.h_outs, L.alloc));
+    DeviceGuard g(k.device);
+    k.zc = k.h_obs_d && k.h_outs_d && zc_same_on(k.device, env->h_obs) && zc_same_on(k.device, k.h_outs) &&
+           !std::getenv("COG_NO_ZEROCOPY");
+    if (k.zc && (rc = dmalloc(&k.mir, cog::publish_mirror_bytes(k.n, L.alloc)))) return rc;
+    k.mir_valid = false;
   }
   env->host = true;
   return refresh_full(env);
@@ -673,6 +775,43 @@ int cog_env_time_encode(cog_env *env, int iters, int variant, double *ms_per_lau
   return COG_OK;
 }
 
+int cog_time_copy(int device, size_t bytes, int iters, double *gb_per_s) {
+  if (iters < 1 || bytes < 16 || !gb_per_s) return fail(COG_ERR_INVALID, "bad argument");
+  bytes &= ~(size_t)15;
+  int cnt = 0;
+  if (hipGetDeviceCount(&cnt) != hipSuccess || device < 0 || device >= cnt) return fail(COG_ERR_NODEVICE, "no HIP device");
+  DeviceGuard g(device);
+  void *a = nullptr, *b = nullptr;
+  hipStream_t st = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc = COG_OK;
+  if (hipMalloc(&a, bytes) != hipSuccess || hipMalloc(&b, bytes) != hipSuccess) rc = fail(COG_ERR_OOM, "copy buffers");
+  if (!rc && (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+              hipEventCreate(&e1) != hipSuccess || hipMemsetAsync(a, 1, bytes, st) != hipSuccess))
+    rc = fail(COG_ERR_HIP, "copy setup");
+  double best = 0.0;
+  for (int v = 0; v < 4 && !rc; v++) {                    // the fastest of the four variants
+    if (cog::launch_copy_peak(a, b, bytes, st, v)) rc = fail(COG_ERR_HIP, "copy launch failed");   // warm-up
+    if (rc) break;
+    (void)hipEventRecord(e0, st);
+    for (int r = 0; r < iters && !rc; r++)
+      if (cog::launch_copy_peak(a, b, bytes, st, v)) rc = fail(COG_ERR_HIP, "copy launch failed");
+    (void)hipEventRecord(e1, st);
+    float ms = 0.f;
+    if (!rc && (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess))
+      rc = fail(COG_ERR_HIP, "copy timing");
+    if (!rc) best = std::max(best, 2.0 * (double)bytes * iters / ((double)ms * 1e-3) / 1e9);
+  }
+  if (!rc) *gb_per_s = best;
+  if (st) (void)hipStreamSynchronize(st);
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (st) (void)hipStreamDestroy(st);
+  if (a) (void)hipFree(a);
+  if (b) (void)hipFree(b);
+  return rc;
+}
+
 void *cog_env_stream(cog_env *env) { return env ? (void *)env->sh[0].stream : nullptr; }
 void *cog_env_shard_stream(cog_env *env, int k) {
   if (!env || k < 0 || (size_t)k >= env->sh.size()) return nullptr;
@@ -716,7 +855,7 @@ int cog_sampler_create_multi(size_t n_envs, uint64_t seed, const int *devices, i
   if (rc) return rc;
   cog_sampler *s = new cog_sampler();
   s->n = n_envs;
-  if ((rc = hmalloc(&s->h_actions, n_envs * COG_ACTION_BYTES))) {
+  if ((rc = zc_alloc(&s->h_actions, n_envs * COG_ACTION_BYTES))) {
     sampler_free(s);
     return rc;
   }
@@ -770,9 +909,11 @@ int cog_sampler_num_shards(const cog_sampler *s, int *out) {
 
 static int sampler_run(SamplerShard &k, cog_action_t *h_actions, const uint8_t *d_masks, hipStream_t stream,
                        bool host_refresh) {
-  if (cog::launch_sample(k.n, d_masks, k.d_rng, k.d_actions, stream))
+  uint8_t *h_act = host_refresh && k.n ? const_cast<uint8_t *>(zc_device(h_actions + k.first, k.n * COG_ACTION_BYTES)) : nullptr;
+  if (h_act && !zc_same_on(k.device, h_actions)) h_act = nullptr;
+  if (cog::launch_sample(k.n, d_masks, k.d_rng, k.d_actions, stream, h_act))   // actions to the host view in place
     return fail(COG_ERR_HIP, std::string("sample launch failed: ") + hipGetErrorString(hipGetLastError()));
-  if (host_refresh && k.n)
+  if (host_refresh && k.n && !h_act)
     HIPCHK(hipMemcpyAsync(h_actions + k.first, k.d_actions, k.n * COG_ACTION_BYTES, hipMemcpyDeviceToHost, stream));
   return COG_OK;
 }
@@ -795,8 +936,12 @@ int cog_sampler_sample(cog_sampler *s, const cog_action_mask_t *masks, size_t n)
   for (SamplerShard &k : s->sh) {
     if (!k.n) continue;
     DeviceGuard g(k.device);
-    HIPCHK(hipMemcpyAsync(k.d_masks, masks + k.first, k.n * COG_MASK_BYTES, hipMemcpyHostToDevice, k.stream));
-    int rc = sampler_run(k, s->h_actions, k.d_masks, k.stream, true);
+    const uint8_t *dm = zc_device(masks + k.first, k.n * COG_MASK_BYTES);   // read in place when pinned
+    if (!dm || !zc_same_on(k.device, masks + k.first)) {
+      HIPCHK(hipMemcpyAsync(k.d_masks, masks + k.first, k.n * COG_MASK_BYTES, hipMemcpyHostToDevice, k.stream));
+      dm = k.d_masks;
+    }
+    int rc = sampler_run(k, s->h_actions, dm, k.stream, true);
     if (rc) return rc;
   }
   for (SamplerShard &k : s->sh) {
@@ -945,7 +1090,7 @@ int cog_runner_sync(cog_runner *r) {
   int rc = runner_flush_sample(r);
   if (rc) return rc;
   const bool host = !(r->flags & COG_RUNNER_DEVICE_VIEWS);
-  if (host) {
+  if (host && !r->env->host) {                       // no env views yet: the sampler's view alone
     for (size_t j = 0; j < r->env->sh.size(); j++) {
       EnvShard &k = r->env->sh[j];
       SamplerShard &q = r->smp->sh[j];
@@ -955,7 +1100,7 @@ int cog_runner_sync(cog_runner *r) {
                             k.stream));
     }
   }
-  return finish(r->env, host);
+  return finish(r->env, host, host && r->env->host ? r->smp : nullptr);   // (the actions ride with the env's views)
 }
 
 int cog_runner_set_chunk(cog_runner *r, int steps_per_launch) {

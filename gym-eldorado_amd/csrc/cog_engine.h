@@ -120,11 +120,19 @@ int launch_reset(const DevState &s, const ResetParams &p, void *stream);
 int launch_encode_all(const DevState &s, void *stream, int variant = 0);
 int launch_step(const DevState &s, const uint8_t *d_actions, void *stream);
 int launch_sample(size_t n, const uint8_t *d_masks, uint32_t *d_rng, uint8_t *d_actions,
-                  void *stream);
+                  void *stream, uint8_t *h_actions = nullptr);   // h_actions: device-mapped host view (or null)
+// the host views' dynamic records from HBM: granules that differ from `mir` (an HBM copy of the
+// host views) are stored into the device-mapped pinned views h_obs / h_outs (and into mir);
+// outs_bytes a multiple of 16; force = 1 stores every granule; d_actions / h_actions optional
+int launch_publish(const DevState &s, const uint8_t *outs, uint8_t *mir, uint8_t *h_obs, uint8_t *h_outs,
+                   size_t outs_bytes, int force, const uint8_t *d_actions, uint8_t *h_actions, void *stream);
+size_t publish_mirror_bytes(size_t n, size_t outs_bytes);
 int launch_sample_step(const DevState &s, int mask_source, uint32_t *d_rng, uint8_t *d_actions,
                        void *stream);
 int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions,
                    void *stream);                    // persistent K-step runner loop
 int launch_seed_sampler(size_t n, uint64_t seed, size_t first, uint32_t *d_rng, void *stream);
+// variant bit 0: non-temporal loads/stores; bit 1: 32 waves per CU instead of 8; bytes: a multiple of 16
+int launch_copy_peak(const void *src, void *dst, size_t bytes, void *stream, int variant);
 
 }  // namespace cog

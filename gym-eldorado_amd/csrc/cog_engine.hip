@@ -2176,8 +2176,11 @@ __global__ void __launch_bounds__(NL) k_env_rollout(DevState s, int steps, uint3
 }
 
 
+// masks may be device memory or pinned host memory (zero-copy); h_actions (may be null) is the
+// host view of the actions, written straight over PCIe beside the device copy
 __global__ void __launch_bounds__(256) k_sample(size_t n, const uint8_t *__restrict__ masks,
-                                                uint32_t *__restrict__ rngs, uint8_t *__restrict__ actions) {
+                                                uint32_t *__restrict__ rngs, uint8_t *__restrict__ actions,
+                                                uint8_t *__restrict__ h_actions) {
   __shared__ UidEntry tab[kUidTab];
   uid_tab_fill(tab);
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2187,6 +2190,45 @@ __global__ void __launch_bounds__(256) k_sample(size_t n, const uint8_t *__restr
   sample_mask(masks + i * COG_MASK_BYTES, rng, a, tab);
   rngs[i] = rng;
   store_action(actions + i * COG_ACTION_BYTES, a);
+  if (h_actions) store_action(h_actions + i * COG_ACTION_BYTES, a);
+}
+
+// Host views without copy commands: the dynamic part of every host-visible record -- the ObsData
+// tail (phase, resources, shop, decks, stored masks: granules 1008..1075 of each 1,076-granule
+// record) and the shard's outs block (status, selected masks, info, rewards, dones, agents) -- is
+// compared granule by granule with `mir`, an HBM copy of what the host views hold, and only the
+// granules that differ are stored over PCIe into the pinned host views (and into `mir`).  The
+// status granules always go.  A step changes about 200 of the 1,490 bytes per env, so PCIe
+// carries the changes instead of a full refresh, and one kernel replaces the D2H copy commands
+// (each costs 10-15 us of latency; a 2-D copy of the tails measured 15.7-140 us for 256 envs,
+// depending on the box).  force = 1 stores everything (the host views' state is unknown).  The
+// sampler's actions (the 8 bytes store_action writes at the head of each 64-B record) ride along
+// when act is given.
+constexpr size_t kRecG = COG_OBS_BYTES / 16, kTail0 = COG_OBS_MAP_BYTES / 16, kTailG = kRecG - kTail0;
+__global__ void __launch_bounds__(256) k_publish(const uint4 *__restrict__ obs, const uint4 *__restrict__ outs,
+                                                 uint4 *__restrict__ mir, uint4 *__restrict__ h_obs,
+                                                 uint4 *__restrict__ h_outs, size_t n, size_t outs_g, int force,
+                                                 const uint2 *__restrict__ act, uint2 *__restrict__ h_act) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t tail = n * kTailG;
+  if (t < tail) {
+    const size_t row = t / kTailG, a = row * kRecG + kTail0 + (t - kTailG * row);
+    const uint4 c = obs[a];
+    if (force || ne4(c, mir[t])) {
+      h_obs[a] = c;
+      mir[t] = c;
+    }
+  } else if (t < tail + outs_g) {
+    const size_t u = t - tail;
+    const uint4 c = outs[u];
+    if (force || u < 4 || ne4(c, mir[t])) {
+      h_outs[u] = c;
+      mir[t] = c;
+    }
+  } else if (act && t < tail + outs_g + n) {
+    const size_t i = t - tail - outs_g;
+    h_act[(COG_ACTION_BYTES / 8) * i] = act[(COG_ACTION_BYTES / 8) * i];
+  }
 }
 
 __global__ void k_sync_heads(DevState s) {
@@ -2197,6 +2239,35 @@ __global__ void k_sync_heads(DevState s) {
 __global__ void k_seed_sampler(size_t n, uint64_t seed, size_t first, uint32_t *rngs) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) rngs[i] = mr_seed(seed + (uint64_t)(first + i));   // vec_sampler.h:9-13 (no u32 wrap)
+}
+
+// The measured device copy peak beside which the encode's HBM fraction is reported (BASELINE.md
+// "plus a measured copy-kernel peak"): 16-B loads and stores (plain or non-temporal), 4 granules
+// in flight per work-item, a grid striding over the buffer; cog_time_copy reports the faster.
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+template <bool NT>
+DEV u32x4_t cp_ld(const u32x4_t *p) {
+  if (NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
+template <bool NT>
+DEV void cp_st(u32x4_t v, u32x4_t *p) {
+  if (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+template <bool NT>
+__global__ void __launch_bounds__(256) k_copy_peak(const u32x4_t *__restrict__ src, u32x4_t *__restrict__ dst, size_t n16) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const u32x4_t a = cp_ld<NT>(src + i), b = cp_ld<NT>(src + i + stride);
+    const u32x4_t c = cp_ld<NT>(src + i + 2 * stride), d = cp_ld<NT>(src + i + 3 * stride);
+    cp_st<NT>(a, dst + i);
+    cp_st<NT>(b, dst + i + stride);
+    cp_st<NT>(c, dst + i + 2 * stride);
+    cp_st<NT>(d, dst + i + 3 * stride);
+  }
+  for (; i < n16; i += stride) cp_st<NT>(cp_ld<NT>(src + i), dst + i);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2233,9 +2304,11 @@ int launch_step(const DevState &s, const uint8_t *d_actions, void *stream) {
                      d_actions, nullptr, nullptr);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-int launch_sample(size_t n, const uint8_t *d_masks, uint32_t *d_rng, uint8_t *d_actions, void *stream) {
+int launch_sample(size_t n, const uint8_t *d_masks, uint32_t *d_rng, uint8_t *d_actions, void *stream,
+                  uint8_t *h_actions) {
   if (!n) return 0;
-  hipLaunchKernelGGL(k_sample, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, n, d_masks, d_rng, d_actions);
+  hipLaunchKernelGGL(k_sample, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, n, d_masks, d_rng, d_actions,
+                     h_actions);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_sample_step(const DevState &s, int mask_source, uint32_t *d_rng, uint8_t *d_actions, void *stream) {
@@ -2263,6 +2336,25 @@ int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rn
   // envs (round 2).  The kernel's register allocation (about 490 VGPRs + AGPRs per work-item)
   // admits one wave per SIMD, so 2,048 half-empty waves ran in two rounds on 1,024 SIMDs
   rollout_launch<64>(s, mask_source, steps, d_rng, d_actions, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int launch_publish(const DevState &s, const uint8_t *outs, uint8_t *mir, uint8_t *h_obs, uint8_t *h_outs, size_t outs_bytes,
+                   int force, const uint8_t *d_actions, uint8_t *h_actions, void *stream) {
+  if (!s.n) return 0;
+  const size_t outs_g = outs_bytes / 16, threads = s.n * kTailG + outs_g + (d_actions ? s.n : 0);
+  hipLaunchKernelGGL(k_publish, dim3(blocks_for(threads, 256)), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const uint4 *>(s.obs), reinterpret_cast<const uint4 *>(outs),
+                     reinterpret_cast<uint4 *>(mir), reinterpret_cast<uint4 *>(h_obs), reinterpret_cast<uint4 *>(h_outs),
+                     s.n, outs_g, force, reinterpret_cast<const uint2 *>(d_actions), reinterpret_cast<uint2 *>(h_actions));
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+size_t publish_mirror_bytes(size_t n, size_t outs_bytes) { return n * kTailG * 16 + outs_bytes; }
+int launch_copy_peak(const void *src, void *dst, size_t bytes, void *stream, int variant) {
+  const u32x4_t *a = static_cast<const u32x4_t *>(src);
+  u32x4_t *b = static_cast<u32x4_t *>(dst);
+  const dim3 g(variant & 2 ? 8192 : 2048), t(256);   // 8 or 32 waves per CU
+  if (variant & 1) hipLaunchKernelGGL(k_copy_peak<true>, g, t, 0, (hipStream_t)stream, a, b, bytes / 16);
+  else hipLaunchKernelGGL(k_copy_peak<false>, g, t, 0, (hipStream_t)stream, a, b, bytes / 16);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_seed_sampler(size_t n, uint64_t seed, size_t first, uint32_t *d_rng, void *stream) {

@@ -146,6 +146,11 @@ COG_API int cog_env_signal_stream(cog_env *env, int shard, void *stream);
  * times back to back; average device time per launch (HIP events).  Output is unchanged.
  * variant: 0 = production kernel, >0 = alternative implementations kept for A/B timing. */
 COG_API int cog_env_time_encode(cog_env *env, int iters, int variant, double *ms_per_launch);
+/* measurement: read + write bytes per second of the engine's device copy kernel (16-B loads and
+ * stores, plain or non-temporal, 8 or 32 waves per CU: the fastest) over two `bytes` buffers on
+ * `device`: the copy peak beside which the encode's HBM fraction is reported (BASELINE.md "a
+ * measured copy-kernel peak") */
+COG_API int cog_time_copy(int device, size_t bytes, int iters, double *gb_per_s);
 COG_API int cog_env_device(const cog_env *env); /* device ordinal */
 /* on (default): a finished env is reset inside the same step call, as vec_cog_env<N>::step does
  * (vec_environment.h:56-59).  off: cog_env::step semantics (environment.cpp:91-95) -- the env
