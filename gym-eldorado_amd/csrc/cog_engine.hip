@@ -584,31 +584,6 @@ DEV void add_players(const Ctx &e) {                       // map.cpp:343-354 (Q
   if (start == COG_PIECE_START0 + 1 && n < 4) pv->flags |= F_B_START_LT4;
 }
 
-// cog_env::reset() (environment.cpp:42-64)
-DEV bool env_reset(const Ctx &e) {
-  EnvPriv *pv = e.pv;
-  pv->agent = 0;
-  e.sh[0] = COG_PHASE_INACTIVE;
-  map_reset(e);
-  GenScratch *gs = e.gs;
-  for (int p = 0; p < COG_N_PIECES; p++) { gs->pcx[p] = 0; gs->pcy[p] = 0; gs->prot[p] = 0; }
-  if (!generate(e)) {
-    pv->flags |= F_MAPGEN_FAIL;
-    return false;
-  }
-  build_cgrid(e);
-  for (int i = 0; i < pv->n_players; i++) player_reset(e, i);
-  add_players(e);
-  for (int k = 0; k < COG_N_SHOP; k++) e.sh[SH_SHOP + k] = COG_CARDS_PER_TYPE;
-  pv->in_market = kInMarket0;                              // n_in_market NOT reset (Q12)
-  pv->done = 0;
-  pv->turn_counter = 0;
-  for (int i = 0; i < pv->n_players; i++) update_observation(e, i);
-  copy_mask(e.sel, stm(e, 0));
-  for (int i = 0; i < pv->n_players; i++) load_cells(e, i);
-  return true;
-}
-
 // done: Info + rewards (environment.cpp:187-207, get_reward :281-288)
 DEV void finish_episode(const Ctx &e) {
   EnvPriv *pv = e.pv;
@@ -703,6 +678,516 @@ DEV void wave_encode(const DevState &s, size_t i, bool enc) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Wave-cooperative map generation.  generate() above is the reference's algorithm one env per
+// work-item: a long divergent chain of dependent grid loads (k_reset: 9.4 ms for 65,536 maps,
+// 96 % of it in generate; one auto-reset inside a rollout stalls its wave for ~180 us).  Here the
+// whole wave generates ONE env's map at a time: the generation state is wave-uniform (every lane
+// holds the same value), the placed-piece list and the piece transforms are spread over lanes,
+// and Map::add_random_piece's candidate placements are tested lane-parallel -- lane c checks
+// candidate c's footprint with all its grid loads in flight at once -- and counted / selected
+// by ballot + popcount, so the reference's two passes over the candidate list (count, draw, find
+// the chosen one) cost one round of loads.  Same algorithm, same RNG draws, same candidate order
+// (map.cpp:277-307), same hazards; the owner lane then finishes the reset (players, shop, masks).
+// ------------------------------------------------------------------------------------------
+DEV uint32_t nth_set_bit(uint32_t m, uint32_t j);
+// Lanes of the wave read what other lanes stored: wait until the wave's stores have completed
+// (a workgroup fence compiles to nothing for one-wave workgroups), then invalidate the CU's vector
+// L1 (an agent-scope acquire: buffer_inv sc1), which may still hold a line loaded before those
+// stores -- measured: without it, candidate footprints read hexes placed earlier in the same
+// generation as empty
+DEV void wg_fence() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+DEV int lane_id() { return (int)(threadIdx.x & 63u); }
+DEV int rdl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }   // l wave-uniform
+DEV int wave_min(int v) {
+#pragma unroll
+  for (int o = 32; o; o >>= 1) v = min(v, __shfl_xor(v, o));
+  return v;
+}
+DEV int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+// rot_pt as a linear map: rotation t sends (X, Y) to X*u + Y*v; u, v components + 1 packed in
+// 2-bit fields (ux, uy, vx, vy) per t
+constexpr uint32_t rot_uv_code(int ux, int uy, int vx, int vy) {
+  return (uint32_t)(ux + 1) | (uint32_t)(uy + 1) << 2 | (uint32_t)(vx + 1) << 4 | (uint32_t)(vy + 1) << 6;
+}
+constexpr uint32_t kRotUV[6] = {rot_uv_code(1, 0, 0, 1), rot_uv_code(0, 1, -1, 1), rot_uv_code(-1, 1, -1, 0),
+                                rot_uv_code(-1, 0, 0, -1), rot_uv_code(0, -1, 1, -1), rot_uv_code(1, -1, 1, 0)};
+constexpr uint64_t kRotUVPack = (uint64_t)kRotUV[0] | (uint64_t)kRotUV[1] << 8 | (uint64_t)kRotUV[2] << 16 |
+                                (uint64_t)kRotUV[3] << 24 | (uint64_t)kRotUV[4] << 32 | (uint64_t)kRotUV[5] << 40;
+struct RotUV {
+  int ux, uy, vx, vy;
+};
+DEV RotUV rot_uv(int t) {                                   // t in [0, 6)
+  const uint32_t f = (uint32_t)(kRotUVPack >> (8 * t)) & 0xffu;
+  return RotUV{(int)(f & 3u) - 1, (int)((f >> 2) & 3u) - 1, (int)((f >> 4) & 3u) - 1, (int)(f >> 6) - 1};
+}
+constexpr bool rot_uv_ok() {                                // against rot_pt's six cases
+  for (int t = 0; t < 6; t++) {
+    const uint32_t f = kRotUV[t];
+    const int ux = (int)(f & 3u) - 1, uy = (int)((f >> 2) & 3u) - 1, vx = (int)((f >> 4) & 3u) - 1, vy = (int)(f >> 6) - 1;
+    const int X = 3, Y = 5;                                 // any point: the maps are linear
+    const int ex[6] = {X, -Y, -X - Y, -X, Y, X + Y}, ey[6] = {Y, X + Y, X, -Y, -X - Y, -X};
+    if (X * ux + Y * vx != ex[t] || X * uy + Y * vy != ey[t]) return false;
+  }
+  return true;
+}
+static_assert(rot_uv_ok(), "rotation table");
+DEV int norm6_small(int v) {                                // v in [-6, 12)
+  v = v < 0 ? v + 6 : v;
+  return v >= 6 ? v - 6 : v;
+}
+
+constexpr int8_t kLargeXY[37][2] = COG_LARGE_XY2;
+constexpr int8_t kSmallXY[16][2] = COG_SMALL_XY2;
+constexpr int8_t kEndXY[3][2] = COG_END_XY2;
+// connection sets (conn_set): 0 LARGE->LARGE, 1 LARGE->SMALL, 2 LARGE->TRIPLE, 3 SMALL->LARGE;
+// their base points flattened (set s starts at kConnOff[s]), packed as bytes
+constexpr int8_t kConnX[12] = {8, 6, 3, 5, 7, 0, -7, -5, -3, 7, 5, 3};
+constexpr int8_t kConnY[12] = {6, 8, 7, 5, 3, 8, 10, 10, 10, -10, -10, -10};
+constexpr bool conn_tables_ok() {
+  const int8_t ll[2][2] = COG_CONN_LL_XY2, ls[3][2] = COG_CONN_LS_XY2, lt[1][2] = COG_CONN_LT_XY2,
+               sl[6][2] = COG_CONN_SL_XY2;
+  for (int j = 0; j < 2; j++) if (kConnX[j] != ll[j][0] || kConnY[j] != ll[j][1]) return false;
+  for (int j = 0; j < 3; j++) if (kConnX[2 + j] != ls[j][0] || kConnY[2 + j] != ls[j][1]) return false;
+  if (kConnX[5] != lt[0][0] || kConnY[5] != lt[0][1]) return false;
+  for (int j = 0; j < 6; j++) if (kConnX[6 + j] != sl[j][0] || kConnY[6 + j] != sl[j][1]) return false;
+  return true;
+}
+static_assert(conn_tables_ok(), "connection tables");
+constexpr uint64_t pack8lo(const int8_t *v) {
+  uint64_t r = 0;
+  for (int k = 0; k < 8; k++) r |= (uint64_t)(uint8_t)v[k] << (8 * k);
+  return r;
+}
+constexpr uint32_t pack8hi(const int8_t *v) {
+  uint32_t r = 0;
+  for (int k = 0; k < 4; k++) r |= (uint32_t)(uint8_t)v[8 + k] << (8 * k);
+  return r;
+}
+constexpr uint64_t kConnXLo = pack8lo(kConnX), kConnYLo = pack8lo(kConnY);
+constexpr uint32_t kConnXHi = pack8hi(kConnX), kConnYHi = pack8hi(kConnY);
+DEV int conn_coord(uint64_t lo, uint32_t hi, int k) {      // signed byte k of the packed table
+  const uint32_t b = k < 8 ? (uint32_t)(lo >> (8 * k)) : (hi >> (8 * (k - 8)));
+  return (int)(int8_t)(b & 0xffu);
+}
+DEV int conn_off(int set) { return set == 0 ? 0 : set == 1 ? 2 : set == 2 ? 5 : 6; }
+DEV int conn_nbase(int set) { return set == 0 ? 2 : set == 1 ? 3 : set == 2 ? 1 : 6; }
+DEV int conn_copies(int set) { return set == 3 ? 1 : 7; }
+DEV int conn_opt0(int set) { return set == 1 ? -1 : set == 2 ? -3 : -2; }
+DEV int conn_nopt(int set) { return set == 1 ? 2 : set == 2 ? 1 : 6; }
+DEV int conn_opt(int set, uint32_t ri) { return set == 1 ? (ri ? 2 : -1) : set == 2 ? -3 : (int)ri - 2; }
+// conn_set(q, psize) as a set id, -1: q offers nothing to a piece of size psize
+DEV int conn_set_id(int q, int psize) {
+  const int qs = c_pmeta[q].size, qk = c_pmeta[q].kind;
+  if (qs == COG_PS_LARGE) {
+    if (psize == COG_PS_LARGE) return 0;
+    if (psize == COG_PS_SMALL) return 1;
+    if (psize == COG_PS_TRIPLE && qk != COG_PT_START) return 2;
+    return -1;
+  }
+  return (qs == COG_PS_SMALL && psize == COG_PS_LARGE) ? 3 : -1;
+}
+
+struct GenW {                         // wave-uniform generation state of one env
+  uint8_t *grid;
+  int minx, miny, maxx, maxy, dimx, dimy;
+  uint32_t flags;                     // EnvPriv::flags (sticky: read at entry, written back)
+  int np;                             // pieces placed
+  int pl0, pl1;                       // lane k: pieces[k], pieces[64 + k]
+  int tx, ty, tr;                     // lane q < COG_N_PIECES: pcx[q], pcy[q], prot[q]
+};
+DEV int placed(const GenW &W, int qi) { return qi < 64 ? rdl(W.pl0, qi) : rdl(W.pl1, qi - 64); }
+
+DEV void coop_map_reset(GenW &W) {                         // map.cpp:744-752
+  for (int x = W.minx; x <= W.maxx; x++)
+    for (int y = W.miny + lane_id(); y <= W.maxy; y += 64) W.grid[(x + kGridOff) * kGridDim + (y + kGridOff)] = 0;
+  W.minx = W.miny = W.maxx = W.maxy = 0;
+  W.dimx = W.dimy = 0;
+  W.np = 0;
+  wg_fence();
+}
+
+// add_piece (map.cpp:179-191, 309-341): lane k places hex k; the first failing hex (off the
+// lattice / past kMaxCoord) stops the placement with the hexes before it written, as in order
+DEV bool coop_add_piece(GenW &W, int p, int cx2, int cy2, int rot) {
+  const int lane = lane_id();
+  int r = rdl(W.tr, p) + rot;
+  r %= 6;
+  r = r < 0 ? r + 6 : r;
+  const int pcx = rdl(W.tx, p) + cx2, pcy = rdl(W.ty, p) + cy2;
+  if (lane == p) {
+    W.tr = r;
+    W.tx = pcx;
+    W.ty = pcy;
+  }
+  if (W.np >= kMaxPlaced) {
+    W.flags |= F_GRID_OVER;
+    return false;
+  }
+  if (W.np < 64) {
+    if (lane == W.np) W.pl0 = p;
+  } else if (lane == W.np - 64) {
+    W.pl1 = p;
+  }
+  W.np++;
+  const int nh = c_pmeta[p].n_hex;
+  const bool in = lane < nh;
+  int X, Y;
+  piece_xy2(p, in ? lane : 0, X, Y);
+  const RotUV R = rot_uv(r);
+  const int rx = X * R.ux + Y * R.vx + pcx, ry = X * R.uy + Y * R.vy + pcy;
+  const int x = rx >> 1, y = ry >> 1;                      // exact: only used when both are even
+  const bool bad = ((rx | ry) & 1) || x < -kMaxCoord || x > kMaxCoord || y < -kMaxCoord || y > kMaxCoord;
+  const uint64_t bm = __builtin_amdgcn_ballot_w64(in && bad);
+  const int f = bm ? __ffsll((unsigned long long)bm) - 1 : nh;
+  if (lane < f) W.grid[(x + kGridOff) * kGridDim + (y + kGridOff)] = c_phex[p][lane];
+  wg_fence();
+  if (bm) {
+    W.flags |= F_GRID_OVER;
+    return false;
+  }
+  W.minx = min(W.minx, wave_min(in ? x : W.minx));
+  W.miny = min(W.miny, wave_min(in ? y : W.miny));
+  W.maxx = max(W.maxx, wave_max(in ? x : W.maxx));
+  W.maxy = max(W.maxy, wave_max(in ? y : W.maxy));
+  return true;
+}
+
+// footprint_free for this lane's candidate: every hex's grid load issued before any is used
+template <int NH>
+DEV bool footprint_hit(const uint8_t *grid, const int8_t (*xy)[2], int t, int cx2, int cy2) {
+  const RotUV R = rot_uv(t);
+  uint32_t v[NH];
+  bool on[NH];
+#pragma unroll
+  for (int k = 0; k < NH; k++) {
+    const int X = xy[k][0], Y = xy[k][1];
+    const int rx = X * R.ux + Y * R.vx + cx2, ry = X * R.uy + Y * R.vy + cy2;
+    const int x = rx >> 1, y = ry >> 1;
+    on[k] = !((rx | ry) & 1) && x >= -kGridOff && x < kGridOff && y >= -kGridOff && y < kGridOff;
+    v[k] = grid[on[k] ? (x + kGridOff) * kGridDim + (y + kGridOff) : 0];
+  }
+  bool hit = false;
+#pragma unroll
+  for (int k = 0; k < NH; k++) hit |= on[k] && v[k] != 0u;
+  return hit;
+}
+
+struct Cand {                         // candidate c of add_random_piece's enumeration order
+  int set, q, ci, j;
+};
+// candidate c (c < total) -> (placed piece, copy, base point), in map.cpp:282-300's loop order
+DEV Cand cand_of(const GenW &W, int psize, int c) {
+  Cand k{-1, 0, 0, 0};
+  int acc = 0, local = 0;
+  for (int qi = 0; qi < W.np; qi++) {
+    const int q = placed(W, qi);
+    const int set = conn_set_id(q, psize);
+    const int n = set < 0 ? 0 : conn_copies(set) * conn_nbase(set);
+    if (c >= acc && c < acc + n) {
+      k.set = set;
+      k.q = q;
+      local = c - acc;
+    }
+    acc += n;
+  }
+  const int nb = conn_nbase(k.set);
+  k.ci = k.set == 0 ? local >> 1 : k.set == 1 ? (local * 171) >> 9 : k.set == 2 ? local : 0;   // local / nb (< 21)
+  k.j = local - k.ci * nb;
+  return k;
+}
+// the candidate's centre and the rotation its footprint is tested at
+DEV void cand_place(const GenW &W, const Cand &k, bool uniform_q, int &cx, int &cy, int &t, int &qrot) {
+  int qcx, qcy;
+  if (uniform_q) {
+    qrot = rdl(W.tr, k.q); qcx = rdl(W.tx, k.q); qcy = rdl(W.ty, k.q);
+  } else {
+    qrot = __shfl(W.tr, k.q); qcx = __shfl(W.tx, k.q); qcy = __shfl(W.ty, k.q);
+  }
+  const int b = conn_off(k.set) + k.j;
+  const int bx = conn_coord(kConnXLo, kConnXHi, b), by = conn_coord(kConnYLo, kConnYHi, b);
+  const RotUV R = rot_uv(norm6_small(k.ci + qrot));
+  cx = bx * R.ux + by * R.vx + qcx;
+  cy = bx * R.uy + by * R.vy + qcy;
+  t = norm6_small(conn_opt0(k.set) + k.ci + qrot);
+}
+// this lane's candidate (c = batch * 64 + lane) is a valid placement of piece p.  Every lane
+// runs it (a lane past the end evaluates candidate 0): the transforms are read from other lanes
+// (ds_bpermute), and an inactive source lane would read as 0
+DEV bool cand_free(const GenW &W, int p, int psize, int c, int total) {
+  const Cand k = cand_of(W, psize, c < total ? c : 0);
+  int cx, cy, t, qrot;
+  cand_place(W, k, false, cx, cy, t, qrot);
+  bool hit;
+  if (psize == COG_PS_LARGE) hit = footprint_hit<37>(W.grid, kLargeXY, t, cx, cy);
+  else if (psize == COG_PS_SMALL) hit = footprint_hit<16>(W.grid, kSmallXY, t, cx, cy);
+  else hit = footprint_hit<3>(W.grid, kEndXY, t, cx, cy);
+  if (c >= total) return false;
+  return !hit;
+}
+DEV int nth_set_bit64(uint64_t m, uint32_t j) {
+  const uint32_t lo = (uint32_t)m, c = __popc(lo);
+  return j < c ? (int)nth_set_bit(lo, j) : 32 + (int)nth_set_bit((uint32_t)(m >> 32), j - c);
+}
+
+// Map::add_random_piece (map.cpp:277-307)
+DEV bool coop_add_random_piece(GenW &W, int p, uint32_t &rng) {
+  const int lane = lane_id();
+  if (lane == p) {                                         // MapPiece::reset
+    W.tx = 0;
+    W.ty = 0;
+    W.tr = 0;
+  }
+  const int psize = c_pmeta[p].size;
+  int total = 0;
+  for (int qi = 0; qi < W.np; qi++) {
+    const int set = conn_set_id(placed(W, qi), psize);
+    total += set < 0 ? 0 : conn_copies(set) * conn_nbase(set);
+  }
+  uint64_t bal0 = 0, bal1 = 0;                             // the first two batches' ballots
+  uint32_t nvalid = 0;
+  for (int b = 0; b * 64 < total; b++) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(cand_free(W, p, psize, b * 64 + lane, total));
+    if (b == 0) bal0 = m;
+    if (b == 1) bal1 = m;
+    nvalid += (uint32_t)__popcll(m);
+  }
+  if (!nvalid) return false;
+  const uint32_t chosen = uid(rng, nvalid);
+  int c = 0;
+  uint32_t acc = 0;
+  for (int b = 0; b * 64 < total; b++) {
+    const uint64_t m = b == 0 ? bal0 : b == 1 ? bal1 : __builtin_amdgcn_ballot_w64(cand_free(W, p, psize, b * 64 + lane, total));
+    const uint32_t pc = (uint32_t)__popcll(m);
+    if (chosen < acc + pc) {
+      c = b * 64 + nth_set_bit64(m, chosen - acc);
+      break;
+    }
+    acc += pc;
+  }
+  const Cand k = cand_of(W, psize, c);
+  int cx, cy, t, qrot;
+  cand_place(W, k, true, cx, cy, t, qrot);
+  const uint32_t ri = uid(rng, (uint32_t)conn_nopt(k.set));
+  return coop_add_piece(W, p, cx, cy, conn_opt(k.set, ri) + k.ci + qrot);
+}
+
+DEV bool coop_finalize_ok(GenW &W) {                       // map.cpp:389-405 (dims check, Q27)
+  const int dx = 3 + W.maxx - W.minx, dy = 3 + W.maxy - W.miny;
+  if (dx > 49 || dy > 49) {
+    W.flags |= F_GRID_OVER;
+    return false;
+  }
+  W.dimx = dx;
+  W.dimy = dy;
+  return true;
+}
+
+constexpr uint32_t travel_mask(int diff) {                 // travel pieces of difficulty <= diff
+  const uint8_t d[COG_N_TRAVEL] = {0, 1, 2, 0, 2, 1, 1, 0, 1, 1, 2, 1, 2, 1, 1, 1};
+  uint32_t m = 0;
+  for (int i = 0; i < COG_N_TRAVEL; i++) m |= (d[i] <= diff ? 1u : 0u) << i;
+  return m;
+}
+constexpr bool travel_mask_ok() {
+  const cog_piece_meta_t meta[COG_N_PIECES] = COG_PIECE_META;
+  for (int diff = 0; diff < 4; diff++)
+    for (int i = 0; i < COG_N_TRAVEL; i++)
+      if ((((travel_mask(diff) >> i) & 1u) != 0u) != (meta[COG_PIECE_TRAVEL0 + i].difficulty <= diff)) return false;
+  return true;
+}
+static_assert(travel_mask_ok(), "travel piece difficulties");
+
+// generate() on wave-uniform frames: a frame is (rng, next travel index i, the valid list as a
+// bit set -- it starts sorted and erasing keeps it sorted, so valid[k] is the k-th set bit --,
+// stage), held in registers selected by depth
+DEV bool coop_generate_frames(GenW &W, uint32_t rng0, int n_pieces, int diff) {
+  enum { ENTER = 0, LOOP = 1, END = 2, FIN = 3 };
+  uint32_t f_rng[COG_MAX_FAILURES], f_mask[COG_MAX_FAILURES];
+  int f_i[COG_MAX_FAILURES], f_stage[COG_MAX_FAILURES];
+#pragma unroll
+  for (int d = 0; d < COG_MAX_FAILURES; d++) { f_rng[d] = 0; f_mask[d] = 0; f_i[d] = 0; f_stage[d] = ENTER; }
+  f_rng[0] = rng0;
+  int depth = 0;
+  while (depth >= 0) {
+    uint32_t rng = 0, mask = 0;
+    int fi = 0, stage = 0;
+#pragma unroll
+    for (int d = 0; d < COG_MAX_FAILURES; d++)
+      if (d == depth) { rng = f_rng[d]; mask = f_mask[d]; fi = f_i[d]; stage = f_stage[d]; }
+    bool push = false, pop = false;
+    if (stage == ENTER) {
+      const uint32_t s = uid(rng, 2);
+      if (!coop_add_piece(W, COG_PIECE_START0 + (int)s, 0, 0, 0)) return false;
+      mask = travel_mask(diff);
+      fi = 0;
+      stage = LOOP;
+    } else if (stage == LOOP) {
+      if (fi < n_pieces) {
+        bool ok = false;
+        int next = 0;
+        const uint32_t nv = (uint32_t)__popc(mask);
+        if (nv) {
+          next = (int)nth_set_bit(mask, uid(rng, nv));
+          ok = coop_add_random_piece(W, COG_PIECE_TRAVEL0 + next, rng);
+          if (W.flags & F_GRID_OVER) return false;
+        }
+        fi++;
+        if (ok) {                                          // vector::erase(begin() + next), Q5
+          if ((uint32_t)next >= nv) W.flags |= F_ERASE_PAST;   // past the end: the last one goes
+          mask &= ~(1u << nth_set_bit(mask, (uint32_t)next < nv ? (uint32_t)next : nv - 1u));
+        } else {
+          if (depth + 1 >= COG_MAX_FAILURES) return false;
+          push = true;
+        }
+      } else {
+        stage = END;
+      }
+    } else if (stage == END) {
+      const uint32_t en = uid(rng, 2);
+      stage = FIN;
+      const bool ok = coop_add_random_piece(W, COG_PIECE_END0 + (int)en, rng);
+      if (W.flags & F_GRID_OVER) return false;
+      if (!ok) {
+        coop_map_reset(W);
+        if (depth + 1 >= COG_MAX_FAILURES) return false;
+        push = true;
+      }
+    } else {                                               // FIN: finalize, then return
+      if (!coop_finalize_ok(W)) return false;
+      pop = true;
+    }
+#pragma unroll
+    for (int d = 0; d < COG_MAX_FAILURES; d++)
+      if (d == depth) { f_rng[d] = rng; f_mask[d] = mask; f_i[d] = fi; f_stage[d] = stage; }
+    if (push) {                                            // recursion with the frame's rng copy
+#pragma unroll
+      for (int d = 0; d < COG_MAX_FAILURES; d++)
+        if (d == depth + 1) { f_rng[d] = rng; f_stage[d] = ENTER; }
+      depth++;
+    } else if (pop) {
+      depth--;
+    }
+  }
+  return true;
+}
+
+DEV void coop_build_cgrid(const GenW &W, uint8_t *cgrid) {  // build_cgrid, lane k: block k
+  uint4 *out = reinterpret_cast<uint4 *>(cgrid);
+  for (int k = lane_id(); k < kEncBlocks; k += 64) {
+    const int ix = k / 3, iy0 = (k % 3) * 16;
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (ix < W.dimx) {
+      const uint8_t *row = W.grid + (ix - 1 + W.minx + kGridOff) * kGridDim + kGridOff + W.miny - 1;
+#pragma unroll
+      for (int j = 0; j < 16; j++)
+        if (iy0 + j < W.dimy) w[j >> 2] |= (uint32_t)row[iy0 + j] << (8 * (j & 3));
+    }
+    out[k] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+// map_reset + the piece transforms' reset (environment.cpp:46-49), Map::generate and, when it
+// succeeds, the compact code grid, for env `env`, by the whole wave; returns whether generation
+// succeeded.  The EnvPriv / GenScratch fields generation owns are written back at the end.
+// The env's EnvPriv fields generation reads, as the owner lane holds them (it read them itself:
+// program order covers its own earlier stores) and broadcasts them
+struct GenIn {
+  uint32_t rng, flags, bounds, npd;   // bounds: minx, miny, maxx, maxy bytes; npd: n_pieces | difficulty << 8
+};
+DEV GenIn gen_in_of(const EnvPriv *pv) {
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(pv);
+  return GenIn{pv->rng, pv->flags, w[offsetof(EnvPriv, minx) / 4], (uint32_t)pv->n_pieces | (uint32_t)pv->difficulty << 8};
+}
+DEV bool coop_generate(const DevState &s, uint32_t env, int owner, const GenIn &own) {
+  const int lane = lane_id();
+  EnvPriv *pv = s.priv + env;
+  GenScratch *gs = s.gen + env;
+  GenW W;
+  W.grid = s.grid + (size_t)env * kGridBytes;
+  const uint32_t bounds = (uint32_t)rdl((int)own.bounds, owner);
+  W.minx = (int8_t)(bounds & 0xffu); W.miny = (int8_t)((bounds >> 8) & 0xffu);
+  W.maxx = (int8_t)((bounds >> 16) & 0xffu); W.maxy = (int8_t)(bounds >> 24);
+  W.dimx = W.dimy = 0;
+  W.flags = (uint32_t)rdl((int)own.flags, owner);
+  const uint32_t rng0 = (uint32_t)rdl((int)own.rng, owner);
+  const uint32_t npd = (uint32_t)rdl((int)own.npd, owner);
+  const int n_pieces = (int)(npd & 0xffu), diff = (int)(npd >> 8);
+  coop_map_reset(W);
+  W.tx = W.ty = W.tr = 0;
+  W.pl0 = W.pl1 = 0;
+  const bool ok = coop_generate_frames(W, rng0, n_pieces, diff);
+  if (ok) coop_build_cgrid(W, s.cgrid + (size_t)env * COG_CELLS);
+  if (lane == owner) {                                     // what the owner lane reads back later
+    pv->minx = (int8_t)W.minx; pv->miny = (int8_t)W.miny; pv->maxx = (int8_t)W.maxx; pv->maxy = (int8_t)W.maxy;
+    pv->dimx = (uint8_t)W.dimx; pv->dimy = (uint8_t)W.dimy;
+    pv->flags = W.flags;
+    gs->npieces = (uint8_t)W.np;
+    gs->pieces[0] = (uint8_t)rdl(W.pl0, 0);                // (add_players' start piece)
+  }
+  if (lane < COG_N_PIECES) {
+    gs->pcx[lane] = (int16_t)W.tx;
+    gs->pcy[lane] = (int16_t)W.ty;
+    gs->prot[lane] = (uint8_t)W.tr;
+  }
+  if (lane > 0 && lane < W.np) gs->pieces[lane] = (uint8_t)W.pl0;
+  if (64 + lane < W.np) gs->pieces[64 + lane] = (uint8_t)W.pl1;
+  return ok;
+}
+
+// The wave generates, one env after another, the map of every lane whose `want` is set, and
+// returns this lane's result.  Called by every lane of the wave in converged control flow (a
+// wave-uniform no-op when no lane wants a map).  The owner lane reads the EnvPriv fields
+// generation needs and writes back what it reads later itself; the grid and cgrid, which lanes
+// write for each other, are ordered by waits for the wave's stores (wg_fence).
+DEV bool wave_generate(const DevState &s, size_t i, bool want) {
+  uint64_t m = __builtin_amdgcn_ballot_w64(want);
+  if (!m) return false;
+  GenIn own{};
+  if (want) own = gen_in_of(s.priv + i);
+  bool mine = false;
+  while (m) {
+    const int l = __ffsll((unsigned long long)m) - 1;
+    m &= m - 1;
+    const uint32_t env = (uint32_t)rdl((int)(uint32_t)i, l);
+    const bool ok = coop_generate(s, env, l, own);
+    if (lane_id() == l) mine = ok;
+  }
+  wg_fence();
+  return mine;
+}
+
+// cog_env::reset() (environment.cpp:42-64) around the wave's generation: before it ...
+DEV void env_reset_pre(const Ctx &e) {
+  e.pv->agent = 0;
+  e.sh[0] = COG_PHASE_INACTIVE;
+}
+// ... and after it, on the owner lane: players, shop, masks, neighbourhood caches
+DEV bool env_reset_post(const Ctx &e, bool gen_ok) {
+  EnvPriv *pv = e.pv;
+  if (!gen_ok) {
+    pv->flags |= F_MAPGEN_FAIL;
+    return false;
+  }
+  for (int i = 0; i < pv->n_players; i++) player_reset(e, i);
+  add_players(e);
+  for (int k = 0; k < COG_N_SHOP; k++) e.sh[SH_SHOP + k] = COG_CARDS_PER_TYPE;
+  pv->in_market = kInMarket0;                              // n_in_market NOT reset (Q12)
+  pv->done = 0;
+  pv->turn_counter = 0;
+  for (int i = 0; i < pv->n_players; i++) update_observation(e, i);
+  copy_mask(e.sel, stm(e, 0));
+  for (int i = 0; i < pv->n_players; i++) load_cells(e, i);
+  return true;
+}
+
+// ------------------------------------------------------------------------------------------
 // kernels
 // ------------------------------------------------------------------------------------------
 __global__ void k_init(DevState s, uint32_t default_seed) {
@@ -731,20 +1216,25 @@ __global__ void k_init(DevState s, uint32_t default_seed) {
   }
 }
 
-__global__ void k_reset(DevState s, ResetParams p) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= s.n) return;
+__global__ void k_reset(DevState s, ResetParams p) {     // blocks of one wave (64 envs)
+  const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = i0 < s.n;
+  const size_t i = live ? i0 : 0;
   Ctx e = make_ctx(s, i);
   EnvPriv *pv = e.pv;
-  if (p.use_params) {                                      // cog_env::reset(params) :66-77
-    pv->n_players = p.n_players;
-    pv->n_pieces = p.n_pieces;
-    pv->difficulty = p.difficulty;
-    pv->max_steps = p.max_steps;
-    pv->seed = p.seed + (uint32_t)(s.first + i);           // vec_environment.h:41, u32 wrap (Q33)
-    pv->rng = mr_seed(pv->seed);
+  if (live) {
+    if (p.use_params) {                                    // cog_env::reset(params) :66-77
+      pv->n_players = p.n_players;
+      pv->n_pieces = p.n_pieces;
+      pv->difficulty = p.difficulty;
+      pv->max_steps = p.max_steps;
+      pv->seed = p.seed + (uint32_t)(s.first + i);         // vec_environment.h:41, u32 wrap (Q33)
+      pv->rng = mr_seed(pv->seed);
+    }
+    env_reset_pre(e);
   }
-  if (!env_reset(e)) {
+  const bool ok = wave_generate(s, i, live);               // converged: the whole wave
+  if (live && !env_reset_post(e, ok)) {
     atomicOr(&s.status[0], pv->flags);
     atomicAdd(&s.status[1], 1u);
     *s.err = 1u;                                           // host-visible error flag
@@ -1855,32 +2345,42 @@ DEV void step_action(RegEnv &R, const uint8_t *act_in, size_t i, uint32_t &srng,
 }
 
 // episode end + dones[i] + auto-reset (environment.cpp:187-207, vec_environment.h:56-59) on the
-// stored state; returns true when the env's map was regenerated (the wave encodes it)
-// `out` caches (dones[i] | agent_selection[i] << 8) as last stored (~0u: unknown), so bytes that
-// already hold the value are not stored again
-DEV bool end_of_step(const DevState &s, size_t i, bool was_done, bool finish, uint32_t &agent, uint32_t &out) {
+// stored state, in two halves around the wave's map generation (wave_generate, converged):
+// end_of_step_a finishes the episode and stores dones[i]; it returns true when the env
+// auto-resets, and end_of_step_b then completes the reset (true: the map was regenerated, the
+// wave encodes it).  `out` caches (dones[i] | agent_selection[i] << 8) as last stored (~0u:
+// unknown), so bytes that already hold the value are not stored again.
+DEV bool end_of_step_a(const DevState &s, size_t i, bool was_done, bool finish, uint32_t &agent, uint32_t &out) {
   if (finish) finish_episode(make_ctx(s, i));
   const bool done = was_done || finish;
   if ((out & 0xffu) != (done ? 1u : 0u)) s.done[i] = done ? 1 : 0;   // dones[i] before the auto-reset
-  bool enc = false;
   if (done && s.autoreset) {
-    Ctx e = make_ctx(s, i);
-    if (!env_reset(e)) {
-      atomicOr(&s.status[0], e.pv->flags);
-      atomicAdd(&s.status[1], 1u);
-      *s.err = 1u;                                         // host-visible error flag
-    } else {
-      enc = true;
-      if (s.cap) {                                         // host views: list the regenerated maps
-        const uint32_t k = atomicAdd(&s.status[2], 1u);
-        if (k < s.cap) s.dirty[k] = (uint32_t)i;
-      }
-    }
-    sync_heads(s, i);
-    agent = e.pv->agent;
+    env_reset_pre(make_ctx(s, i));
+    out = (out & ~0xffu) | 1u;
+    return true;
   }
   if (((out >> 8) & 0xffu) != (agent & 0xffu)) s.agent[i] = (uint8_t)agent;
   out = (done ? 1u : 0u) | (agent & 0xffu) << 8;
+  return false;
+}
+DEV bool end_of_step_b(const DevState &s, size_t i, bool gen_ok, uint32_t &agent, uint32_t &out) {
+  Ctx e = make_ctx(s, i);
+  bool enc = false;
+  if (!env_reset_post(e, gen_ok)) {
+    atomicOr(&s.status[0], e.pv->flags);
+    atomicAdd(&s.status[1], 1u);
+    *s.err = 1u;                                           // host-visible error flag
+  } else {
+    enc = true;
+    if (s.cap) {                                           // host views: list the regenerated maps
+      const uint32_t k = atomicAdd(&s.status[2], 1u);
+      if (k < s.cap) s.dirty[k] = (uint32_t)i;
+    }
+  }
+  sync_heads(s, i);
+  agent = e.pv->agent;
+  if (((out >> 8) & 0xffu) != (agent & 0xffu)) s.agent[i] = (uint8_t)agent;
+  out = 1u | (agent & 0xffu) << 8;
   return enc;
 }
 
@@ -1888,7 +2388,7 @@ DEV bool end_of_step(const DevState &s, size_t i, bool was_done, bool finish, ui
 // flight), step on registers, store what changed, [finish / auto-reset].
 template <int SRC>
 DEV bool env_step_lane(const DevState &s, size_t i, const uint8_t *act_in, uint32_t *rngs, uint8_t *actions_out,
-                       const UidEntry *tab) {
+                       const UidEntry *tab, uint32_t &agent, uint32_t &out) {
   STAMP(s, 0);
   PH_DECL;
   Snap S;
@@ -1915,10 +2415,11 @@ DEV bool env_step_lane(const DevState &s, size_t i, const uint8_t *act_in, uint3
     store_action(actions_out + i * COG_ACTION_BYTES, act);
   }
   STAMP(s, 3);
-  uint32_t agent = R.agent(), out = ~0u;
-  const bool enc = end_of_step(s, i, was_done, finish, agent, out);
+  agent = R.agent();
+  out = ~0u;
+  const bool rs = end_of_step_a(s, i, was_done, finish, agent, out);
   STAMP(s, 4);
-  return enc;
+  return rs;                                               // the env auto-resets (end_of_step_b)
 }
 
 template <int SRC>
@@ -1926,10 +2427,14 @@ __global__ void __launch_bounds__(64) k_env_step(DevState s, const uint8_t *__re
                                                  uint8_t *__restrict__ actions_out) {
   __shared__ UidEntry tab[kUidTab];
   uid_tab_fill(tab);
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool enc = false;
-  if (i < s.n) enc = env_step_lane<SRC>(s, i, act_in, rngs, actions_out, tab);
-  wave_encode(s, i < s.n ? i : 0, enc);                    // converged: the whole wave encodes
+  const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t i = i0 < s.n ? i0 : 0;
+  bool rs = false, enc = false;
+  uint32_t agent = 0, out = ~0u;
+  if (i0 < s.n) rs = env_step_lane<SRC>(s, i, act_in, rngs, actions_out, tab, agent, out);
+  const bool ok = wave_generate(s, i, rs);                 // converged: the whole wave generates
+  if (rs) enc = end_of_step_b(s, i, ok, agent, out);
+  wave_encode(s, i, enc);                                  // converged: the whole wave encodes
   STAMP(s, 5);
 }
 
@@ -2054,12 +2559,17 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s, int steps, uint32_t
   }
 
   if (FIX) {                                               // step `park`'s episode end
-    bool enc = false;
+    bool enc = false, rs = false;
+    uint32_t agent = 0;
     if (live) {
       t_first = (int)(park & ~kParkFinish) + 1;
-      uint32_t agent = S.g1.y & 0xffu;
+      agent = S.g1.y & 0xffu;
       const bool finish = (park & kParkFinish) != 0u;
-      enc = end_of_step(s, i, !finish, finish, agent, out);
+      rs = end_of_step_a(s, i, !finish, finish, agent, out);
+    }
+    const bool ok = wave_generate(s, i, rs);               // converged: the whole wave generates
+    if (live) {
+      if (rs) enc = end_of_step_b(s, i, ok, agent, out);
       load_env(s, i, S);                                   // reset: reload from the stored state
       lds_fill_players(L, s, i, l);
     }
@@ -2076,7 +2586,8 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s, int steps, uint32_t
   PH_DECL;
   for (int t = FIX ? 1 : 0; t < steps; t++) {
     if (!FIX && !live) break;                              // lean: a parked lane leaves the loop
-    bool enc = false;
+    bool enc = false, ended = false, rs = false;
+    uint32_t agent = 0;
     if (live && t >= t_first) {
       RegEnv R;
       regs_env(R, S);
@@ -2109,7 +2620,7 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s, int steps, uint32_t
       if (na != ag) L.heads[na][l] = mbits_u4(bits_of(R.stn));
 #pragma unroll
       for (int k = 0; k < 7; k++) L.deck[ag][k][l] = make_uint4(R.d[4 * k], R.d[4 * k + 1], R.d[4 * k + 2], R.d[4 * k + 3]);
-      uint32_t agent = R.agent();
+      agent = R.agent();
       Snap N;                                              // the next step's player records
       lds_players(L, l, (int)agent, next_of((int)agent), N);
       PH(3);
@@ -2138,17 +2649,24 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s, int steps, uint32_t
           live = false;
           continue;
         }
-        enc = end_of_step(s, i, was_done, finish, agent, out);
-        load_env(s, i, S);                                 // reset: reload from the stored state
-        lds_fill_players(L, s, i, l);
-        agent = S.g1.y & 0xffu;
-        lds_players(L, l, (int)agent, next_of((int)agent), S);
+        ended = true;
+        rs = end_of_step_a(s, i, was_done, finish, agent, out);
       } else {
-        enc = end_of_step(s, i, false, false, agent, out);
+        end_of_step_a(s, i, false, false, agent, out);
       }
       PH(5);
     }
-    if (FIX) wave_encode(s, i, enc);                       // converged: the whole wave encodes
+    if (FIX) {                                             // converged: the whole wave generates
+      const bool ok = wave_generate(s, i, rs);
+      if (ended) {
+        if (rs) enc = end_of_step_b(s, i, ok, agent, out);
+        load_env(s, i, S);                                 // reload from the stored state
+        lds_fill_players(L, s, i, l);
+        agent = S.g1.y & 0xffu;
+        lds_players(L, l, (int)agent, next_of((int)agent), S);
+      }
+      wave_encode(s, i, enc);                              // converged: the whole wave encodes
+    }
     PH(6);
   }
   if (live) {                                              // env-level private state back to HBM
