@@ -2539,14 +2539,42 @@ DEV void lds_players(const LaneLds &L, int l, int ag, int na, Snap &S) {
 // out of its allocation.  A wave with nothing parked ends after the lean pass (round 1 launched
 // the fix-up as a second kernel: 4.8 us per launch even when it had nothing to do).
 constexpr uint32_t kParkNone = ~0u, kParkFinish = 1u << 31;
+// The records of a wave's envs seen from the wave's first env: a per-wave (scalar) base and a
+// per-lane index below 64, so that record addresses are a scalar base plus a 32-bit lane offset
+// (the saddr form of global loads and stores) instead of 64-bit products of a global index,
+// which the compiler rematerialises at every store under the kernel's register pressure.
+DEV DevState wave_view(const DevState &s, size_t base) {
+  DevState v = s;
+  v.obs += base * COG_OBS_BYTES;
+  v.sel += base * COG_MASK_BYTES;
+  v.info += base * COG_INFO_BYTES;
+  v.rew += base * 4;
+  v.done += base;
+  v.agent += base;
+  v.priv += base;
+  v.grid += base * (size_t)kGridBytes;
+  v.cgrid += base * COG_CELLS;
+  v.heads += 5 * base;
+  v.gen += base;
+  v.first += base;
+  v.n = s.n > base ? s.n - base : 0;
+  return v;
+}
 template <int SRC, bool FIX, int NL>
-DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s, int steps, uint32_t *__restrict__ rngs,
-                          uint8_t *__restrict__ actions_out, uint32_t park) {
+DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s_glob, int steps, uint32_t *__restrict__ rngs_glob,
+                          uint8_t *__restrict__ actions_glob, uint32_t park) {
   const int l = threadIdx.x;
-  const size_t i0 = (size_t)blockIdx.x * blockDim.x + l;
-  const size_t i = i0 < s.n ? i0 : 0;
+  const size_t wbase = (size_t)blockIdx.x * blockDim.x;
+  const size_t i0 = wbase + l;
+  // (s, i): the wave's view and the lane's index in it, for every record access; the wave's
+  // generation, its encode and the regenerated-map list take the shard's (s_glob, i_glob)
+  const DevState s = wave_view(s_glob, wbase);
+  const size_t i = (size_t)l;
+  const size_t i_glob = i0 < s_glob.n ? i0 : 0;
+  uint32_t *__restrict__ rngs = rngs_glob + wbase;
+  uint8_t *__restrict__ actions_out = actions_glob + wbase * COG_ACTION_BYTES;
   int t_first = 0;                                         // fix-up: this lane's first full step
-  bool live = i0 < s.n && (!FIX || park != kParkNone);
+  bool live = i0 < s_glob.n && (!FIX || park != kParkNone);
   Snap S;
   uint32_t srng = 0, out = ~0u;                           // out: end_of_step's output cache
   auto next_of = [&](int a) { return a + 1 >= (int)(S.g1.x & 0xffu) ? 0 : a + 1; };   // n_players
@@ -2567,13 +2595,13 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s, int steps, uint32_t
       const bool finish = (park & kParkFinish) != 0u;
       rs = end_of_step_a(s, i, !finish, finish, agent, out);
     }
-    const bool ok = wave_generate(s, i, rs);               // converged: the whole wave generates
+    const bool ok = wave_generate(s_glob, i_glob, rs);               // converged: the whole wave generates
     if (live) {
-      if (rs) enc = end_of_step_b(s, i, ok, agent, out);
+      if (rs) enc = end_of_step_b(s_glob, i_glob, ok, agent, out);
       load_env(s, i, S);                                   // reset: reload from the stored state
       lds_fill_players(L, s, i, l);
     }
-    wave_encode(s, i, enc);                                // converged: the whole wave encodes
+    wave_encode(s_glob, i_glob, enc);                                // converged: the whole wave encodes
   }
   if (live) {
     const int ag = (int)(S.g1.y & 0xffu);
@@ -2657,15 +2685,15 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s, int steps, uint32_t
       PH(5);
     }
     if (FIX) {                                             // converged: the whole wave generates
-      const bool ok = wave_generate(s, i, rs);
+      const bool ok = wave_generate(s_glob, i_glob, rs);
       if (ended) {
-        if (rs) enc = end_of_step_b(s, i, ok, agent, out);
+        if (rs) enc = end_of_step_b(s_glob, i_glob, ok, agent, out);
         load_env(s, i, S);                                 // reload from the stored state
         lds_fill_players(L, s, i, l);
         agent = S.g1.y & 0xffu;
         lds_players(L, l, (int)agent, next_of((int)agent), S);
       }
-      wave_encode(s, i, enc);                              // converged: the whole wave encodes
+      wave_encode(s_glob, i_glob, enc);                              // converged: the whole wave encodes
     }
     PH(6);
   }
