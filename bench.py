@@ -199,14 +199,18 @@ def host_loop(cg, n, difficulty, device, steps, use_runner):
     for _ in range(steps):
         one()
     wall = time.perf_counter() - t0
-    # bytes over PCIe per env-step: D2H ObsData tail (1,088) + selected mask, info, rewards, done,
-    # agent (338) + actions (64); H2D actions (64) [+ masks H2D 128 + actions D2H 64 without runner]
-    d2h = 1088 + 128 + 192 + 16 + 2 + (64 if use_runner else 64)
+    # bytes of host-visible records refreshed per env-step: ObsData tail (1,088) + selected mask,
+    # info, rewards, done, agent (338) + actions (64).  An upper bound of what crosses PCIe:
+    # k_publish stores only the 16-B granules that changed since the last refresh, and the
+    # sampler reads the env's pinned mask view in place
+    d2h = 1088 + 128 + 192 + 16 + 2 + 64
     h2d = 0 if use_runner else 64 + 128
     return {"value": n * steps / wall, "unit": "env-steps/s", "ms_per_step": wall / steps * 1e3,
             "envs": n, "steps": steps, "d2h_bytes_per_env_step": d2h, "h2d_bytes_per_env_step": h2d,
             "survey_8d_writeback_bytes": WRITEBACK_BYTES,
-            "pcie_GBs": n * (d2h + h2d) * steps / wall / 1e9,
+            "view_refresh_GBs_nominal": n * (d2h + h2d) * steps / wall / 1e9,
+            "note": "d2h/h2d bytes are the records refreshed per env-step (upper bound): k_publish "
+                    "moves only the changed 16-B granules over PCIe",
             "loop": "runner.sample(); runner.step_sync()" if use_runner else "sampler.sample(masks); env.step(actions)"}
 
 

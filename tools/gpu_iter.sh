@@ -9,6 +9,7 @@ mkdir -p "$OUT"
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/tests.log" 2>&1 && \
 timeout -k 10 120 bash tools/fixedcost.sh 65536 > "$OUT/fixedcost.txt" 2>&1 && \
 timeout -k 10 200 python -u tools/exp_nl.py 65536,8192 64 > "$OUT/timing.txt" 2>&1 && \
+timeout -k 10 120 python -u tools/exp_step.py 65536,8192 >> "$OUT/timing.txt" 2>&1 && \
 timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-extras --no-cpu-baseline > "$OUT/bench20.json" 2> "$OUT/bench20.err"
 rc=$?
 tail -3 "$OUT/tests.log"
