@@ -278,7 +278,7 @@ def roofline(prof, n, k_chunk, launch_s):
                   "note": "800 B/env-step (SURVEY 8d) assumes every step reads its state from HBM; "
                           "the rollout keeps it on-chip, so this rate can exceed the HBM peak"}
     r = (prof or {}).get("k_env_rollout")
-    if r:
+    if r and r.get("valu_per_wave_step"):
         per_ws = r["valu_per_wave_step"]
         achieved = per_ws * waves * k_chunk / launch_s
         out.update(achieved=achieved, frac=achieved / peak, valu_per_wave_step=per_ws,

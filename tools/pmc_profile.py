@@ -87,6 +87,8 @@ def main(specs, envs=65536):
 
 if __name__ == "__main__":
     a = sys.argv[1:]
+    if not [x for x in a if ":" in x]:
+        sys.exit(__doc__)
     envs = 65536
     if "--envs" in a:
         i = a.index("--envs")
