@@ -1401,8 +1401,7 @@ DEV uint8_t pick(uint32_t &rng, uint32_t m) {
 // (probability < 2^-25 per head) redoes the sampling the sequential way, rejections included.
 DEV void sample_heads(const Heads &h, uint32_t &rng, uint8_t out[5], const UidEntry *tab) {
   const uint32_t m[5] = {h.play, h.spec, h.rem, h.move, h.shop};
-  uint32_t x = rng, r[5], k[5];
-  bool risk = false;
+  uint32_t x = rng, r[5], k[5], riskv = 0;
   const UidEntry e0 = tab[__popc(m[0])];                  // head 0's entry, read before the draws
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1411,10 +1410,12 @@ DEV void sample_heads(const Heads &h, uint32_t &rng, uint8_t out[5], const UidEn
     uint32_t xn = x;
     r[j] = mr_next(xn) - 1u;
     x = k[j] ? xn : x;
-    risk |= k[j] != 0u && r[j] >= kSmallSafe;
+    // r >= kSmallSafe  <=>  bit 31 of r + 34 (r < 2^31 - 2); m | -m has bit 31 set iff m != 0:
+    // the flag stays in a vector register (no compare into a scalar mask per head)
+    riskv |= (r[j] + (0x80000000u - kSmallSafe)) & (m[j] | (0u - m[j]));
   }
   __builtin_amdgcn_sched_barrier(0);
-  if (risk) {
+  if (riskv >> 31) {
     uint32_t y = rng;
 #pragma unroll
     for (int j = 0; j < 5; j++) out[j] = pick(y, m[j]);
