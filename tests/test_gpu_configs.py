@@ -138,3 +138,38 @@ def test_full_dynamics_resets_C5_size_subsets(cg, block):
         resets += int(orc.dones.sum())
     assert resets > (hi - lo) // 2
     assert_equal(env, orc, lo, hi, what=f"C5-size full dynamics envs [{lo}, {hi})")
+
+
+def test_full_dynamics_beyond_4gib_of_observations(cg):
+    """Maximum sizes: 262,144 envs hold 4.5 GB of ObsData, so the records of the envs past
+    249,475 lie beyond 2^32 bytes of the observation buffer (and of the map-generation grids):
+    any 32-bit truncation of a record offset would show there.  Full dynamics (stored masks,
+    auto-resets with device map generation) through the device loop; the last 128 envs are
+    read through the DLPack device views and checked against 1-env-per-seed oracle runs."""
+    n, seed, steps = 262144, 31337, 300
+    env = cg.vec.get_vec_env(n)()
+    smp = cg.vec.get_vec_sampler(n)(seed)
+    env.reset(seed, 4, 3, cg.HARD, 30, False)
+    runner = cg.vec.get_runner(n)(env, smp, None, device_views=True, stored_masks=True)
+    runner.set_chunk(60)
+    runner.rollout(steps)
+    runner.sync()
+    lo, hi = n - 128, n
+    assert lo * 17216 > 2 ** 32
+    t = cg.device_tensors(env)
+    got = {nm: t[nm][lo:hi].cpu().numpy() for nm in ("observations", "selected_action_masks", "infos",
+                                                     "rewards", "dones", "agent_selection")}
+    orc, osm = po.OracleVec(hi - lo), po.OracleSampler(hi - lo, seed + lo)
+    orc.reset(seed + lo, 4, 3, 2, 30)                      # env i == a batch seeded seed + i
+    resets = 0
+    for _ in range(steps):
+        osm.sample(po.stored_masks(orc))
+        orc.step(osm.actions)
+        resets += int(orc.dones.sum())
+    assert resets > (hi - lo) // 2
+    for nm, dt in (("observations", po.OBS), ("selected_action_masks", po.MASK), ("infos", po.INFO)):
+        bad = po.named_equal(np.ascontiguousarray(got[nm]).view(dt).reshape(hi - lo), getattr(orc, nm))
+        assert bad is None, f"envs past 4 GiB: {nm}.{bad} differs from the oracle"
+    assert np.array_equal(got["rewards"], orc.rewards)
+    assert np.array_equal(got["dones"].view(np.bool_), orc.dones)
+    assert np.array_equal(got["agent_selection"], orc.agent_selection)
