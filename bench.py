@@ -287,8 +287,10 @@ def roofline(prof, n, k_chunk, launch_s):
                    wait_quads_per_wave_step=r.get("wait_any_per_wave_step"),
                    wave_quads_per_wave_step=r.get("wave_cycles_per_wave_step"),
                    lone_wave_frac=achieved / (peak / 2),
-                   note="one 64-env wave per SIMD: a lone wave issues at most one VALU per 4 cycles "
-                        "(lone_wave_frac is against that cap); profiled at %d envs x %d steps per launch"
+                   issue_frac=(r.get("active_inst_any_per_wave_step") or 0) / max(r.get("wave_cycles_per_wave_step") or 1, 1),
+                   note="one 64-env wave per SIMD: a lone wave issues at most one instruction per 4 cycles "
+                        "(lone_wave_frac: VALU against that cap; issue_frac: quad-cycles issuing any "
+                        "instruction / wave lifetime, PMC); profiled at %d envs x %d steps per launch"
                         % (r.get("envs_per_launch", 0), r.get("steps_per_launch", 0)))
         tr = r.get("bytes_per_step_launch", {})
         key = str(k_chunk)
