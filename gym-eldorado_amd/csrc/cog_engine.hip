@@ -21,6 +21,7 @@
 //                    (runner.h:46-55)
 //   k_sync_heads     mask bit-vectors of every env from its byte records (init / reset)
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include "cog_engine.h"
 #include "cog_tables.h"
@@ -2568,11 +2569,80 @@ DEV DevState wave_view(const DevState &s, size_t base) {
   v.n = s.n > base ? s.n - base : 0;
   return v;
 }
-template <int SRC, bool FIX, int NL>
+// Two-wave rollout for small shards (k_env_rollout_pipe): the stepping wave hands each step's
+// outputs to a second wave of its workgroup through a double-buffered LDS ring, and the second
+// wave issues the store phase (mask expansions and the granule stores) while the first runs the
+// next step.  One record per lane and step, [buffer][granule][lane]:
+//   0-2  ObsData 16128.. (phase, resources, shop)      3-9  the acting player's DeckObs
+//   10   selected-mask bits, .w = flags: bits 0-2 / 3-9 changed sh / deck granules, 10-15 /
+//        16-21 / 22-27 changed granules of the selected / acting / next player's byte masks,
+//        28 valid, 29 moved, 30 next player != acting player
+//   11   acting player's stored-mask bits, .w = ag | na << 8 | Info steps byte << 16
+//   12   next player's stored-mask bits               13   the action (8 bytes)
+//   14   EnvPriv granule 2 (locations) when moved
+constexpr int kOutG = 15;
+struct OutRing {
+  uint4 g[2][kOutG][64];
+};
+DEV void out_record_write(OutRing &O, int b, int l, int ag, int na, const Snap &S, const RegEnv &R,
+                          const uint8_t act[5]) {
+  uint32_t gm = 1u << 28 | (R.moved ? 1u << 29 : 0u) | (na != ag ? 1u << 30 : 0u);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const uint4 v = make_uint4(R.sh[4 * k], R.sh[4 * k + 1], R.sh[4 * k + 2], R.sh[4 * k + 3]);
+    if (ne4(v, S.sh[k])) gm |= 1u << k;
+    O.g[b][k][l] = v;
+  }
+#pragma unroll
+  for (int k = 0; k < 7; k++) {
+    const uint4 v = make_uint4(R.d[4 * k], R.d[4 * k + 1], R.d[4 * k + 2], R.d[4 * k + 3]);
+    if (ne4(v, S.dk[k])) gm |= 1u << (3 + k);
+    O.g[b][3 + k][l] = v;
+  }
+  const MBits bs = bits_of(R.sel), ba = bits_of(R.sta), bn = bits_of(R.stn);
+  gm |= mask_diff_granules(bs, S.sel) << 10 | mask_diff_granules(ba, S.sta) << 16 |
+        (na != ag ? mask_diff_granules(bn, S.stn) << 22 : 0u);
+  O.g[b][10][l] = make_uint4(bs.w0, bs.w1, bs.w2, gm);
+  O.g[b][11][l] = make_uint4(ba.w0, ba.w1, ba.w2,
+                             (uint32_t)ag | (uint32_t)na << 8 | ((R.info_steps >> (8 * ag)) & 0xffu) << 16);
+  O.g[b][12][l] = make_uint4(bn.w0, bn.w1, bn.w2, 0u);
+  O.g[b][13][l] = make_uint4((uint32_t)act[0] | (uint32_t)act[1] << 8 | (uint32_t)act[2] << 16 | (uint32_t)act[3] << 24,
+                             (uint32_t)act[4], 0u, 0u);
+  O.g[b][14][l] = R.g2;
+}
+// the storing wave: exactly the stores store_outputs + store_action issue, in the same order
+DEV void out_record_store(const OutRing &O, int b, int l, const DevState &s, size_t i, uint8_t *actions_out) {
+  const uint4 m = O.g[b][10][l];
+  const uint32_t gm = m.w;
+  if (!((gm >> 28) & 1u)) return;
+  const uint4 x = O.g[b][11][l];
+  const int ag = (int)(x.w & 0xffu), na = (int)((x.w >> 8) & 0xffu);
+  uint8_t *ob = s.obs + i * COG_OBS_BYTES;
+  s.info[i * COG_INFO_BYTES + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag] = (uint8_t)(x.w >> 16);
+  if ((gm >> 29) & 1u) reinterpret_cast<uint4 *>(s.priv + i)[2] = O.g[b][14][l];
+#pragma unroll
+  for (int k = 0; k < 3; k++)
+    if ((gm >> k) & 1u) reinterpret_cast<uint4 *>(ob + COG_OBS_PHASE)[k] = O.g[b][k][l];
+  uint8_t *deck = deck_ptr(s, i, ag);
+#pragma unroll
+  for (int k = 0; k < 7; k++)
+    if ((gm >> (3 + k)) & 1u) reinterpret_cast<uint4 *>(deck)[k] = O.g[b][3 + k][l];
+  store_mask_record(reinterpret_cast<uint4 *>(s.sel + i * COG_MASK_BYTES), MBits{m.x, m.y, m.z}, (gm >> 10) & 63u);
+  store_mask_record(reinterpret_cast<uint4 *>(deck + COG_PD_MASK), MBits{x.x, x.y, x.z}, (gm >> 16) & 63u);
+  if ((gm >> 30) & 1u) {
+    const uint4 y = O.g[b][12][l];
+    store_mask_record(reinterpret_cast<uint4 *>(deck_ptr(s, i, na) + COG_PD_MASK), MBits{y.x, y.y, y.z},
+                      (gm >> 22) & 63u);
+  }
+  const uint4 a = O.g[b][13][l];
+  reinterpret_cast<uint2 *>(actions_out + i * COG_ACTION_BYTES)[0] = make_uint2(a.x, a.y);
+}
+
+template <int SRC, bool FIX, int NL, bool PIPE = false>
 DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s_glob, int steps, uint32_t *__restrict__ rngs_glob,
-                          uint8_t *__restrict__ actions_glob, uint32_t park) {
-  const int l = threadIdx.x;
-  const size_t wbase = (size_t)blockIdx.x * blockDim.x;
+                          uint8_t *__restrict__ actions_glob, uint32_t park, OutRing *O = nullptr) {
+  const int l = threadIdx.x;                               // (the stepping wave: threads 0..NL-1)
+  const size_t wbase = (size_t)blockIdx.x * NL;
   const size_t i0 = wbase + l;
   // (s, i): the wave's view and the lane's index in it, for every record access; the wave's
   // generation, its encode and the regenerated-map list take the shard's (s_glob, i_glob)
@@ -2621,7 +2691,11 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s_glob, int steps, uin
   __builtin_amdgcn_s_waitcnt(0);
   PH_DECL;
   for (int t = FIX ? 1 : 0; t < steps; t++) {
-    if (!FIX && !live) break;                              // lean: a parked lane leaves the loop
+    if (PIPE) {                                            // every lane, every step: the records
+      if (t) __syncthreads();                              // of step t - 1 to the storing wave
+      if (!live) O->g[t & 1][10][l] = make_uint4(0u, 0u, 0u, 0u);   // (no record)
+    }
+    if (!FIX && !PIPE && !live) break;                     // lean: a parked lane leaves the loop
     bool enc = false, ended = false, rs = false;
     uint32_t agent = 0;
     if (live && t >= t_first) {
@@ -2661,8 +2735,12 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s_glob, int steps, uin
       lds_players(L, l, (int)agent, next_of((int)agent), N);
       PH(3);
 #ifndef COG_ABLATE_STORES                                  // diagnostic timing builds only
-      store_outputs(s, i, ag, na, S, R);
-      store_action(actions_out + i * COG_ACTION_BYTES, act);
+      if (PIPE) {
+        out_record_write(*O, t & 1, l, ag, na, S, R, act);
+      } else {
+        store_outputs(s, i, ag, na, S, R);
+        store_action(actions_out + i * COG_ACTION_BYTES, act);
+      }
 #endif
       PH(4);
       // the next step's image: registers (env level) and the player records just read
@@ -2705,6 +2783,7 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s_glob, int steps, uin
     }
     PH(6);
   }
+  if (PIPE && steps > 0) __syncthreads();                 // the last step's records
   if (live) {                                              // env-level private state back to HBM
     store_env_private(s, i, S);                            // (the player records: lds_store_wave)
     rngs[i] = srng;
@@ -2726,6 +2805,45 @@ __global__ void __launch_bounds__(NL) k_env_rollout(DevState s, int steps, uint3
   __syncthreads();
 #ifndef COG_ABLATE_EPI                                     // diagnostic timing builds only
   lds_store_wave<LaneLds<NL>, NL>(L, s, base, ne);
+#endif
+}
+
+// Shards of <= 32,768 envs leave SIMDs idle (one 64-env wave per SIMD at most): each workgroup
+// gets a second wave for its store phase (OutRing above).  Barriers: one at the start, one per
+// step (the stepping wave hands over step t - 1 at the top of step t, the last step after its
+// loop), one when the storing wave's stores have completed, one before the epilogue.  The fix-up
+// pass (episode ends, resets) then runs on the stepping wave alone with the plain store phase,
+// after an L1 invalidate, since it reloads records the storing wave wrote.
+template <int SRC>
+__global__ void __launch_bounds__(128) k_env_rollout_pipe(DevState s, int steps, uint32_t *__restrict__ rngs,
+                                                          uint8_t *__restrict__ actions_out) {
+  __shared__ LaneLds<64> L;
+  __shared__ OutRing O;
+  const size_t base = (size_t)blockIdx.x * 64;
+  const int ne = (int)min((size_t)64, s.n - base);
+  const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform
+  uid_tab_fill(L.tab);
+  uint32_t park = kParkNone;
+  if (role == 0) {
+    park = rollout_pass<SRC, false, 64, true>(L, s, steps, rngs, actions_out, kParkNone, &O);
+    __syncthreads();                                       // the storing wave's stores are done
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");     // (drop L1 lines they replaced)
+    if (__builtin_amdgcn_ballot_w64(park != kParkNone))    // (wave-uniform)
+      rollout_pass<SRC, true, 64>(L, s, steps, rngs, actions_out, park);
+  } else {
+    const int l = (int)threadIdx.x - 64;
+    const DevState v = wave_view(s, base);
+    uint8_t *av = actions_out + base * COG_ACTION_BYTES;
+    for (int t = 0; t < steps; t++) {
+      __syncthreads();
+      if (l < ne) out_record_store(O, t & 1, l, v, (size_t)l, av);
+    }
+    __builtin_amdgcn_s_waitcnt(0);                         // every store of this wave completed
+    __syncthreads();
+  }
+  __syncthreads();
+#ifndef COG_ABLATE_EPI                                     // diagnostic timing builds only
+  if (role == 0) lds_store_wave<LaneLds<64>, 64>(L, s, base, ne);
 #endif
 }
 
@@ -2884,12 +3002,29 @@ static void rollout_launch(const DevState &s, int mask_source, int steps, uint32
   else
     hipLaunchKernelGGL((k_env_rollout<MASK_SELECTED, NL>), g, b, 0, st, s, steps, d_rng, d_actions);
 }
+// shards up to this size take the two-wave rollout; $COG_ROLLOUT_PIPE_MAX overrides it (0: never)
+static size_t pipe_max_envs() {
+  static const size_t v = [] {
+    const char *e = getenv("COG_ROLLOUT_PIPE_MAX");
+    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)32768;
+  }();
+  return v;
+}
 int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions, void *stream) {
   if (!s.n || steps <= 0) return 0;
   // one 64-env wave per workgroup: 32-env workgroups measured 7.3 us/step against 3.8 at 65,536
   // envs (round 2).  The kernel's register allocation (about 490 VGPRs + AGPRs per work-item)
   // admits one wave per SIMD, so 2,048 half-empty waves ran in two rounds on 1,024 SIMDs
-  rollout_launch<64>(s, mask_source, steps, d_rng, d_actions, (hipStream_t)stream);
+  const hipStream_t st = (hipStream_t)stream;
+  if (s.n <= pipe_max_envs()) {                            // SIMDs to spare: the two-wave form
+    const dim3 g(blocks_for(s.n, 64)), b(128);
+    if (mask_source == MASK_STORED)
+      hipLaunchKernelGGL((k_env_rollout_pipe<MASK_STORED>), g, b, 0, st, s, steps, d_rng, d_actions);
+    else
+      hipLaunchKernelGGL((k_env_rollout_pipe<MASK_SELECTED>), g, b, 0, st, s, steps, d_rng, d_actions);
+  } else {
+    rollout_launch<64>(s, mask_source, steps, d_rng, d_actions, st);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_publish(const DevState &s, const uint8_t *outs, uint8_t *mir, uint8_t *h_obs, uint8_t *h_outs, size_t outs_bytes,
