@@ -364,8 +364,9 @@ def main():
         extras["shard_sizes"] = {"us_per_step_at_%d" % n: launch_s / k_chunk * 1e6 if k_chunk >= 1000 else
                                  us_per_step(cg, n, dev),
                                  "us_per_step_at_%d" % N_SHARD8: us_per_step(cg, N_SHARD8, dev),
-                                 "note": "rollout device time per step, 1,000-step launches; the N=8 shard "
-                                         "(8,192 envs = 128 waves) runs one wave per CU on half the CUs"}
+                                 "note": "rollout device time per step, 1,000-step launches; shards of <= 32,768 "
+                                         "envs (the N=8 shard: 8,192 = 128 workgroups) take the two-wave "
+                                         "rollout, a second wave per workgroup issuing the store phase"}
         # one kernel launch per step (the runner's step() path)
         pl_steps = 500
         runner.set_chunk(1)
