@@ -11,7 +11,8 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.txt" 2>&1 && \
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 > "$OUT/bench20.json" 2> "$OUT/bench20.err" && \
 timeout -k 10 300 python bench.py --no-cpu-baseline > "$OUT/bench_default.json" 2> "$OUT/bench_default.err" && \
-bash tools/profile_round.sh "$TAG/prof" > "$OUT/prof.log" 2>&1
+bash tools/profile_round.sh "$TAG/prof" > "$OUT/prof.log" 2>&1 && \
+timeout -k 10 200 python -u tools/exp_nl.py 65536,32768,16384,8192 64 > "$OUT/shard_sizes.txt" 2>&1
 rc=$?
 tail -3 "$OUT/tests.log"
 cat "$OUT/smoke.txt"
