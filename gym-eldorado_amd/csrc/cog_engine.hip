@@ -2571,16 +2571,17 @@ DEV DevState wave_view(const DevState &s, size_t base) {
 }
 // Two-wave rollout for small shards (k_env_rollout_pipe): the stepping wave hands each step's
 // outputs to a second wave of its workgroup through a double-buffered LDS ring, and the second
-// wave issues the store phase (mask expansions and the granule stores) while the first runs the
-// next step.  One record per lane and step, [buffer][granule][lane]:
-//   0-2  ObsData 16128.. (phase, resources, shop)      3-9  the acting player's DeckObs
-//   10   selected-mask bits, .w = flags: bits 0-2 / 3-9 changed sh / deck granules, 10-15 /
-//        16-21 / 22-27 changed granules of the selected / acting / next player's byte masks,
-//        28 valid, 29 moved, 30 next player != acting player
-//   11   acting player's stored-mask bits, .w = ag | na << 8 | Info steps byte << 16
-//   12   next player's stored-mask bits               13   the action (8 bytes)
-//   14   EnvPriv granule 2 (locations) when moved
-constexpr int kOutG = 15;
+// wave finds what changed and issues the store phase (mask expansions and the granule stores)
+// while the first runs the next step.  One record per lane and step, [buffer][granule][lane]:
+//   0-2   ObsData 16128.. (phase, resources, shop) after the step, 3-5 before it
+//   6-12  the acting player's DeckObs after the step
+//   13    selected-mask bits after, .w = flags: bits 0-6 changed deck granules (the stepping wave
+//         holds the deck's previous value), 28 valid, 29 moved, 30 next player != acting player
+//   14    acting player's stored-mask bits after, .w = ag | na << 8 | Info steps byte << 16
+//   15    next player's stored-mask bits after
+//   16-18 the three mask bit vectors before the step (9 dwords), then the action (8 bytes)
+//   19    EnvPriv granule 2 (locations) when moved
+constexpr int kOutG = 20;
 struct OutRing {
   uint4 g[2][kOutG][64];
 };
@@ -2589,53 +2590,57 @@ DEV void out_record_write(OutRing &O, int b, int l, int ag, int na, const Snap &
   uint32_t gm = 1u << 28 | (R.moved ? 1u << 29 : 0u) | (na != ag ? 1u << 30 : 0u);
 #pragma unroll
   for (int k = 0; k < 3; k++) {
-    const uint4 v = make_uint4(R.sh[4 * k], R.sh[4 * k + 1], R.sh[4 * k + 2], R.sh[4 * k + 3]);
-    if (ne4(v, S.sh[k])) gm |= 1u << k;
-    O.g[b][k][l] = v;
+    O.g[b][k][l] = make_uint4(R.sh[4 * k], R.sh[4 * k + 1], R.sh[4 * k + 2], R.sh[4 * k + 3]);
+    O.g[b][3 + k][l] = S.sh[k];
   }
 #pragma unroll
   for (int k = 0; k < 7; k++) {
     const uint4 v = make_uint4(R.d[4 * k], R.d[4 * k + 1], R.d[4 * k + 2], R.d[4 * k + 3]);
-    if (ne4(v, S.dk[k])) gm |= 1u << (3 + k);
-    O.g[b][3 + k][l] = v;
+    if (ne4(v, S.dk[k])) gm |= 1u << k;
+    O.g[b][6 + k][l] = v;
   }
   const MBits bs = bits_of(R.sel), ba = bits_of(R.sta), bn = bits_of(R.stn);
-  gm |= mask_diff_granules(bs, S.sel) << 10 | mask_diff_granules(ba, S.sta) << 16 |
-        (na != ag ? mask_diff_granules(bn, S.stn) << 22 : 0u);
-  O.g[b][10][l] = make_uint4(bs.w0, bs.w1, bs.w2, gm);
-  O.g[b][11][l] = make_uint4(ba.w0, ba.w1, ba.w2,
+  O.g[b][13][l] = make_uint4(bs.w0, bs.w1, bs.w2, gm);
+  O.g[b][14][l] = make_uint4(ba.w0, ba.w1, ba.w2,
                              (uint32_t)ag | (uint32_t)na << 8 | ((R.info_steps >> (8 * ag)) & 0xffu) << 16);
-  O.g[b][12][l] = make_uint4(bn.w0, bn.w1, bn.w2, 0u);
-  O.g[b][13][l] = make_uint4((uint32_t)act[0] | (uint32_t)act[1] << 8 | (uint32_t)act[2] << 16 | (uint32_t)act[3] << 24,
-                             (uint32_t)act[4], 0u, 0u);
-  O.g[b][14][l] = R.g2;
+  O.g[b][15][l] = make_uint4(bn.w0, bn.w1, bn.w2, 0u);
+  O.g[b][16][l] = make_uint4(S.sel.w0, S.sel.w1, S.sel.w2, S.sta.w0);
+  O.g[b][17][l] = make_uint4(S.sta.w1, S.sta.w2, S.stn.w0, S.stn.w1);
+  O.g[b][18][l] = make_uint4(S.stn.w2,
+                             (uint32_t)act[0] | (uint32_t)act[1] << 8 | (uint32_t)act[2] << 16 | (uint32_t)act[3] << 24,
+                             (uint32_t)act[4], 0u);
+  O.g[b][19][l] = R.g2;
 }
 // the storing wave: exactly the stores store_outputs + store_action issue, in the same order
 DEV void out_record_store(const OutRing &O, int b, int l, const DevState &s, size_t i, uint8_t *actions_out) {
-  const uint4 m = O.g[b][10][l];
+  const uint4 m = O.g[b][13][l];
   const uint32_t gm = m.w;
   if (!((gm >> 28) & 1u)) return;
-  const uint4 x = O.g[b][11][l];
+  const uint4 x = O.g[b][14][l], o0 = O.g[b][16][l], o1 = O.g[b][17][l], o2 = O.g[b][18][l];
   const int ag = (int)(x.w & 0xffu), na = (int)((x.w >> 8) & 0xffu);
   uint8_t *ob = s.obs + i * COG_OBS_BYTES;
   s.info[i * COG_INFO_BYTES + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag] = (uint8_t)(x.w >> 16);
-  if ((gm >> 29) & 1u) reinterpret_cast<uint4 *>(s.priv + i)[2] = O.g[b][14][l];
+  if ((gm >> 29) & 1u) reinterpret_cast<uint4 *>(s.priv + i)[2] = O.g[b][19][l];
 #pragma unroll
-  for (int k = 0; k < 3; k++)
-    if ((gm >> k) & 1u) reinterpret_cast<uint4 *>(ob + COG_OBS_PHASE)[k] = O.g[b][k][l];
+  for (int k = 0; k < 3; k++) {
+    const uint4 v = O.g[b][k][l];
+    if (ne4(v, O.g[b][3 + k][l])) reinterpret_cast<uint4 *>(ob + COG_OBS_PHASE)[k] = v;
+  }
   uint8_t *deck = deck_ptr(s, i, ag);
 #pragma unroll
   for (int k = 0; k < 7; k++)
-    if ((gm >> (3 + k)) & 1u) reinterpret_cast<uint4 *>(deck)[k] = O.g[b][3 + k][l];
-  store_mask_record(reinterpret_cast<uint4 *>(s.sel + i * COG_MASK_BYTES), MBits{m.x, m.y, m.z}, (gm >> 10) & 63u);
-  store_mask_record(reinterpret_cast<uint4 *>(deck + COG_PD_MASK), MBits{x.x, x.y, x.z}, (gm >> 16) & 63u);
+    if ((gm >> k) & 1u) reinterpret_cast<uint4 *>(deck)[k] = O.g[b][6 + k][l];
+  const MBits bs{m.x, m.y, m.z}, ba{x.x, x.y, x.z};
+  store_mask_record(reinterpret_cast<uint4 *>(s.sel + i * COG_MASK_BYTES), bs,
+                    mask_diff_granules(bs, MBits{o0.x, o0.y, o0.z}));
+  store_mask_record(reinterpret_cast<uint4 *>(deck + COG_PD_MASK), ba, mask_diff_granules(ba, MBits{o0.w, o1.x, o1.y}));
   if ((gm >> 30) & 1u) {
-    const uint4 y = O.g[b][12][l];
-    store_mask_record(reinterpret_cast<uint4 *>(deck_ptr(s, i, na) + COG_PD_MASK), MBits{y.x, y.y, y.z},
-                      (gm >> 22) & 63u);
+    const uint4 y = O.g[b][15][l];
+    const MBits bn{y.x, y.y, y.z};
+    store_mask_record(reinterpret_cast<uint4 *>(deck_ptr(s, i, na) + COG_PD_MASK), bn,
+                      mask_diff_granules(bn, MBits{o1.z, o1.w, o2.x}));
   }
-  const uint4 a = O.g[b][13][l];
-  reinterpret_cast<uint2 *>(actions_out + i * COG_ACTION_BYTES)[0] = make_uint2(a.x, a.y);
+  reinterpret_cast<uint2 *>(actions_out + i * COG_ACTION_BYTES)[0] = make_uint2(o2.y, o2.z);
 }
 
 template <int SRC, bool FIX, int NL, bool PIPE = false>
@@ -2693,7 +2698,7 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s_glob, int steps, uin
   for (int t = FIX ? 1 : 0; t < steps; t++) {
     if (PIPE) {                                            // every lane, every step: the records
       if (t) __syncthreads();                              // of step t - 1 to the storing wave
-      if (!live) O->g[t & 1][10][l] = make_uint4(0u, 0u, 0u, 0u);   // (no record)
+      if (!live) O->g[t & 1][13][l] = make_uint4(0u, 0u, 0u, 0u);   // (no record)
     }
     if (!FIX && !PIPE && !live) break;                     // lean: a parked lane leaves the loop
     bool enc = false, ended = false, rs = false;

@@ -5,7 +5,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "gym-eldorado_amd"))
+sys.path.insert(0, os.environ.get("COG_PKG_ROOT") or os.path.join(ROOT, "gym-eldorado_amd"))
 import city_of_gold as cg  # noqa: E402
 
 
