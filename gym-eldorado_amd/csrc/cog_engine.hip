@@ -2575,8 +2575,8 @@ DEV DevState wave_view(const DevState &s, size_t base) {
 // while the first runs the next step.  One record per lane and step, [buffer][granule][lane]:
 //   0-2   ObsData 16128.. (phase, resources, shop) after the step, 3-5 before it
 //   6-12  the acting player's DeckObs after the step
-//   13    selected-mask bits after, .w = flags: bits 0-6 changed deck granules (the stepping wave
-//         holds the deck's previous value), 28 valid, 29 moved, 30 next player != acting player
+//   13    selected-mask bits after, .w = flags: 28 valid, 29 moved, 30 next player != acting
+//         player (the storing wave keeps every player's deck as last stored, DeckImage)
 //   14    acting player's stored-mask bits after, .w = ag | na << 8 | Info steps byte << 16
 //   15    next player's stored-mask bits after
 //   16-18 the three mask bit vectors before the step (9 dwords), then the action (8 bytes)
@@ -2587,18 +2587,14 @@ struct OutRing {
 };
 DEV void out_record_write(OutRing &O, int b, int l, int ag, int na, const Snap &S, const RegEnv &R,
                           const uint8_t act[5]) {
-  uint32_t gm = 1u << 28 | (R.moved ? 1u << 29 : 0u) | (na != ag ? 1u << 30 : 0u);
+  const uint32_t gm = 1u << 28 | (R.moved ? 1u << 29 : 0u) | (na != ag ? 1u << 30 : 0u);
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     O.g[b][k][l] = make_uint4(R.sh[4 * k], R.sh[4 * k + 1], R.sh[4 * k + 2], R.sh[4 * k + 3]);
     O.g[b][3 + k][l] = S.sh[k];
   }
 #pragma unroll
-  for (int k = 0; k < 7; k++) {
-    const uint4 v = make_uint4(R.d[4 * k], R.d[4 * k + 1], R.d[4 * k + 2], R.d[4 * k + 3]);
-    if (ne4(v, S.dk[k])) gm |= 1u << k;
-    O.g[b][6 + k][l] = v;
-  }
+  for (int k = 0; k < 7; k++) O.g[b][6 + k][l] = make_uint4(R.d[4 * k], R.d[4 * k + 1], R.d[4 * k + 2], R.d[4 * k + 3]);
   const MBits bs = bits_of(R.sel), ba = bits_of(R.sta), bn = bits_of(R.stn);
   O.g[b][13][l] = make_uint4(bs.w0, bs.w1, bs.w2, gm);
   O.g[b][14][l] = make_uint4(ba.w0, ba.w1, ba.w2,
@@ -2611,8 +2607,25 @@ DEV void out_record_write(OutRing &O, int b, int l, int ag, int na, const Snap &
                              (uint32_t)act[4], 0u);
   O.g[b][19][l] = R.g2;
 }
+DEV uint4 sel4(bool c, const uint4 &a, const uint4 &b) {
+  return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+}
+// the storing wave's copy of every player's DeckObs as it stands in HBM (loaded at the start of
+// the launch, then updated by its own stores): the previous value of the acting player's deck
+struct DeckImage {
+  uint4 d[4][7];
+};
+DEV void deck_image_load(DeckImage &I, const DevState &s, size_t i) {
+#pragma unroll
+  for (int p = 0; p < 4; p++) {
+    const uint4 *dk = reinterpret_cast<const uint4 *>(deck_ptr(s, i, p));
+#pragma unroll
+    for (int k = 0; k < 7; k++) I.d[p][k] = dk[k];
+  }
+}
 // the storing wave: exactly the stores store_outputs + store_action issue, in the same order
-DEV void out_record_store(const OutRing &O, int b, int l, const DevState &s, size_t i, uint8_t *actions_out) {
+DEV void out_record_store(const OutRing &O, int b, int l, const DevState &s, size_t i, uint8_t *actions_out,
+                          DeckImage &I) {
   const uint4 m = O.g[b][13][l];
   const uint32_t gm = m.w;
   if (!((gm >> 28) & 1u)) return;
@@ -2628,8 +2641,15 @@ DEV void out_record_store(const OutRing &O, int b, int l, const DevState &s, siz
   }
   uint8_t *deck = deck_ptr(s, i, ag);
 #pragma unroll
-  for (int k = 0; k < 7; k++)
-    if ((gm >> k) & 1u) reinterpret_cast<uint4 *>(deck)[k] = O.g[b][6 + k][l];
+  for (int k = 0; k < 7; k++) {
+    const uint4 v = O.g[b][6 + k][l];
+    uint4 old = I.d[3][k];                                 // (selects: a register array indexed
+#pragma unroll                                             // by a lane value would go to scratch)
+    for (int p = 2; p >= 0; p--) old = sel4(ag == p, I.d[p][k], old);
+    if (ne4(v, old)) reinterpret_cast<uint4 *>(deck)[k] = v;
+#pragma unroll
+    for (int p = 0; p < 4; p++) I.d[p][k] = sel4(ag == p, v, I.d[p][k]);
+  }
   const MBits bs{m.x, m.y, m.z}, ba{x.x, x.y, x.z};
   store_mask_record(reinterpret_cast<uint4 *>(s.sel + i * COG_MASK_BYTES), bs,
                     mask_diff_granules(bs, MBits{o0.x, o0.y, o0.z}));
@@ -2839,9 +2859,11 @@ __global__ void __launch_bounds__(128) k_env_rollout_pipe(DevState s, int steps,
     const int l = (int)threadIdx.x - 64;
     const DevState v = wave_view(s, base);
     uint8_t *av = actions_out + base * COG_ACTION_BYTES;
+    DeckImage I;
+    if (l < ne) deck_image_load(I, v, (size_t)l);
     for (int t = 0; t < steps; t++) {
       __syncthreads();
-      if (l < ne) out_record_store(O, t & 1, l, v, (size_t)l, av);
+      if (l < ne) out_record_store(O, t & 1, l, v, (size_t)l, av, I);
     }
     __builtin_amdgcn_s_waitcnt(0);                         // every store of this wave completed
     __syncthreads();
