@@ -31,7 +31,9 @@ Also reported (rank 0; the extra lines only at N=1, so a scaling run stays short
                  shard (8,192, HARD, runner.sample(); runner.step_sync()), D2H bytes per step
   full_dynamics  stored-mask driver (moves, shop, specials), max_steps 30: auto-resets with
                  device map generation inside the rollout
-  reset, sample  time_reset / time_sample equivalents (benchmarks/benchmarks.py:53-69)
+  reset, sample  time_reset / time_sample equivalents (benchmarks/benchmarks.py:53-69); reset()
+                 without arguments beside reset(seed, ...); time_reset_C2 the asv shape (256 EASY)
+  peakmem        asv peakmem_runner: device and host bytes of a runner with host views
   encode         the map-observation encode kernel (reset path), 18,432 B/env, beside a measured
                  device copy peak
   cpu_baseline   the C oracle (port of the reference) on the host cores in the reference
@@ -83,6 +85,7 @@ class Dist:
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.torch = None
         self.pg = False
+        self.device = None
         if self.world > 1:
             import torch
             import torch.distributed as dist
@@ -103,7 +106,7 @@ class Dist:
         stream sync) to the caller, so the clock does not pay for a second synchronisation."""
         t = self.torch
         if t is not None and t.cuda.is_available():
-            t.cuda.synchronize()
+            t.cuda.synchronize(self.device)          # THIS rank's GPU (the engine's device)
         else:
             runner.sync()
         if check:
@@ -131,9 +134,19 @@ class Dist:
 
 
 def device_of(d):
-    """This rank's GPU: LOCAL_RANK, unless COG_DEVICE pins it (several ranks on one GPU)."""
+    """This rank's GPU: LOCAL_RANK, unless COG_DEVICE pins it (several ranks on one GPU) -- the
+    order the library's default device follows (pybind_module.cpp default_devices)."""
     v = os.environ.get("COG_DEVICE")
     return int(v) if v else d.local
+
+
+def bind_device(d, dev):
+    """Make `dev` torch's current device, so that synchronize() and the timing events of this
+    rank cover the GPU its engine runs on (not GPU 0)."""
+    d.device = dev
+    t = d.torch
+    if t is not None and t.cuda.is_available():
+        t.cuda.set_device(dev)
 
 
 def load_profile():
@@ -212,6 +225,63 @@ def host_loop(cg, n, difficulty, device, steps, use_runner):
             "note": "d2h/h2d bytes are the records refreshed per env-step (upper bound): k_publish "
                     "moves only the changed 16-B granules over PCIe",
             "loop": "runner.sample(); runner.step_sync()" if use_runner else "sampler.sample(masks); env.step(actions)"}
+
+
+def time_reset_c2(cg, dev, calls=100):
+    """asv time_reset at the reference's own shape (benchmarks.py:58-62): a 256-env EASY batch,
+    `envs.reset()` without arguments, sequential mode, numpy views live."""
+    n = 256
+    env = cg.vec.get_vec_env(n)(device=dev)
+    env.reset(SEED, N_PLAYERS, N_PIECES, cg.EASY, MAX_STEPS, False)
+    env.observations                                      # host views live, as in the reference
+    env.reset()
+    t1 = time.perf_counter()
+    for _ in range(calls):
+        env.reset()
+    s = (time.perf_counter() - t1) / calls
+    del env
+    return {"envs": n, "calls": calls, "ms_per_call": s * 1e3, "resets_per_s": n / s,
+            "note": "vec_cog_env_256.reset() x calls (asv TimeEnvs.time_reset, sequential)"}
+
+
+def rss_bytes():
+    try:
+        with open("/proc/self/statm") as f:
+            return int(f.read().split()[1]) * os.sysconf("SC_PAGE_SIZE")
+    except Exception:
+        return None
+
+
+def peakmem(cg, d, n, dev):
+    """asv peakmem_runner (benchmarks/benchmarks.py:65-69): the memory a runner holds after one
+    sample + step + sync, here with the reference's host views (numpy) live.  Device bytes are the
+    drop in free HBM (hipMemGetInfo) over env + sampler + runner construction and the first
+    step; host bytes the resident-set growth of this process (pinned views included)."""
+    t = d.torch
+    if t is None or not t.cuda.is_available():
+        return None
+    t.cuda.synchronize(dev)
+    free0 = t.cuda.mem_get_info(dev)[0]
+    rss0 = rss_bytes()
+    env = cg.vec.get_vec_env(n)(device=dev)
+    smp = cg.vec.get_vec_sampler(n)(SEED, device=dev)
+    env.reset(SEED, N_PLAYERS, N_PIECES, cg.HARD, MAX_STEPS, False)
+    runner = cg.vec.get_runner(n)(env, smp, None)
+    views = (env.observations, env.selected_action_masks, env.infos, runner.get_actions())
+    runner.sample()
+    runner.step_sync()
+    t.cuda.synchronize(dev)
+    dev_bytes = free0 - t.cuda.mem_get_info(dev)[0]
+    rss1 = rss_bytes()
+    host = (rss1 - rss0) if rss0 is not None and rss1 is not None else None
+    del views, runner, smp, env
+    # pinned host views: ObsData + selected mask + Info + rewards + done + agent + actions
+    pinned = n * (17216 + 128 + 192 + 16 + 1 + 1 + 64)
+    return {"envs": n, "device_bytes": dev_bytes, "device_bytes_per_env": dev_bytes / n,
+            "host_rss_growth_bytes": host, "host_pinned_view_bytes": pinned,
+            "host_pinned_bytes_per_env": pinned / n,
+            "note": "device: free-HBM drop (granularity of the HIP allocator included); host: RSS growth "
+                    "of the process over the same span, the pinned numpy views included"}
 
 
 def copy_peak_gbs(d):
@@ -312,6 +382,7 @@ def main():
     from city_of_gold.shard import shard, shard_seed
 
     dev = device_of(d)
+    bind_device(d, dev)
     lo, hi = shard(args.envs_total, d.rank, d.world)       # env i of rank r = global index lo + i
     n = hi - lo
     base = shard_seed(SEED, lo)
@@ -425,15 +496,25 @@ def main():
         for _ in range(20):
             smp.sample(masks)
         ss = (time.perf_counter() - t1) / 20
+        t1 = time.perf_counter()
+        for r in range(reps):
+            env.reset()                                   # reset_default: same params, rng continues
+        rd = (time.perf_counter() - t1) / reps
         extras["reset"] = {"envs": n, "s_per_reset_call": rs, "resets_per_s": n / rs,
                            "note": "env.reset(seed, 4, 3, HARD, ...): device map generation + encode + "
-                                   "host views refresh (1.1 GB D2H of ObsData)"}
+                                   "host views refresh (1.1 GB D2H of ObsData)",
+                           "reset_default": {"s_per_call": rd, "resets_per_s": n / rd,
+                                             "note": "env.reset() without arguments, the form asv time_reset "
+                                                     "times (benchmarks.py:58-62): parameters kept, each env's "
+                                                     "rng continues"}}
         extras["sample"] = {"envs": n, "ms_per_call": ss * 1e3, "samples_per_s": n / ss,
                             "note": "sampler.sample(host masks): H2D masks, sampler kernel, D2H actions"}
         del runner, smp, env
         extras["host_loop"] = {
             "C2": host_loop(cg, 256, cg.EASY, dev, 300, False),
             "C4_shard": host_loop(cg, N_SHARD8, cg.HARD, dev, 100, True)}
+        extras["time_reset_C2"] = time_reset_c2(cg, dev)
+        extras["peakmem"] = peakmem(cg, d, n, dev)
 
     if d.rank == 0:
         cpu = None

@@ -75,7 +75,8 @@ def _make_env_cls(n):
         ordered after torch's current stream, or after `stream` (a hipStream_t handle, 0 = the
         null stream; -1: no ordering)."""
         if stream is None:
-            stream = stream_handle()
+            # torch's current stream ON THE ENV'S DEVICE (a stream of another GPU cannot order it)
+            stream = stream_handle(_C.VecEnvBase.shard_info(self, 0)[2])
         _C.VecEnvBase.step_device(self, d_actions, -1 if stream is None else int(stream))
 
     doc = (f"Vectorized city of gold environment for {n} environments.\n\n"
@@ -119,7 +120,7 @@ def _getter(module, prefix, factory):
 DEVICE_VIEWS = ("observations", "selected_action_masks", "rewards", "dones", "agent_selection", "infos")
 
 
-def device_tensors(env, sampler=None, shard=0):
+def device_tensors(env, sampler=None, shard=None):
     """Shard `shard`'s device views (and the sampler's device actions) as torch tensors, zero
     copy via DLPack: rows are records, as uint8 bytes (rewards: float32 (N, 4)).  They alias the
     engine state, which the engine updates on its own HIP stream (env.stream(shard)): before
@@ -129,6 +130,11 @@ def device_tensors(env, sampler=None, shard=0):
     itself with torch's current stream).  The reference's docs suggest TensorDict over copies of
     the numpy views (docs/source/index.rst:20-26); these need no copy."""
     import torch
+    if shard is None:
+        if env.num_shards > 1:
+            raise ValueError(f"device_tensors of a {env.num_shards}-shard env: pass shard=k "
+                             "(each shard's views live on its own GPU)")
+        shard = 0
     out = {nm: torch.from_dlpack(env.dlpack(nm, shard)) for nm in DEVICE_VIEWS}
     if sampler is not None:
         out["actions"] = torch.from_dlpack(sampler.dlpack()) if sampler.num_shards == 1 else None

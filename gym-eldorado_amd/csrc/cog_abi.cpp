@@ -93,6 +93,7 @@ struct ZcRange {
   const uint8_t *base;
   size_t bytes;
   const uint8_t *dev;                 // the device address of base
+  uint64_t same = 0, differs = 0;     // devices (bits) checked to map base at `dev` / elsewhere
 };
 std::mutex g_zc_mu;
 std::vector<ZcRange> g_zc;
@@ -128,12 +129,34 @@ const uint8_t *zc_device(const void *p, size_t bytes) {
     if (r.dev && q >= r.base && q + bytes <= r.base + r.bytes) return r.dev + (q - r.base);
   return nullptr;
 }
-// every device of a multi-GPU handle must see a view at the address recorded at allocation
+// every device of a multi-GPU handle must see a view at the address recorded at allocation;
+// the answer is cached per view and device, so the per-step host calls pay one lookup
 bool zc_same_on(int device, const void *p) {
-  DeviceGuard g(device);
+  const uint8_t *q = static_cast<const uint8_t *>(p);
+  const uint64_t bit = device >= 0 && device < 64 ? 1ull << device : 0;
+  const uint8_t *base = nullptr, *expect = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_zc_mu);
+    for (const ZcRange &r : g_zc)
+      if (r.dev && q >= r.base && q < r.base + r.bytes) {
+        if (r.same & bit) return true;
+        if (r.differs & bit) return false;
+        base = r.base;
+        expect = r.dev;
+        break;
+      }
+  }
+  if (!base) return false;
   void *d = nullptr;
-  if (hipHostGetDevicePointer(&d, const_cast<void *>(p), 0) != hipSuccess) return false;
-  return d == zc_device(p, 1);
+  bool ok;
+  {
+    DeviceGuard g(device);
+    ok = hipHostGetDevicePointer(&d, const_cast<uint8_t *>(base), 0) == hipSuccess && d == expect;
+  }
+  std::lock_guard<std::mutex> lk(g_zc_mu);
+  for (ZcRange &r : g_zc)
+    if (r.base == base) (ok ? r.same : r.differs) |= bit;
+  return ok;
 }
 
 // the reference runner's block split (runner.h:33-38): n / k per block, the last takes the rest
@@ -231,7 +254,8 @@ void env_free(cog_env *e) {
   for (EnvShard &k : e->sh) {
     DeviceGuard g(k.device);
     if (k.stream) (void)hipStreamSynchronize(k.stream);
-    void *dev[] = {k.s.obs, k.outs, k.s.priv, k.s.grid, k.s.cgrid, k.s.heads, k.s.gen, k.s.dirty, k.d_actions, k.mir};
+    void *dev[] = {k.s.obs, k.outs, k.s.priv, k.s.grid, k.s.cgrid, k.s.heads, k.s.gen, k.s.dirty, k.d_actions, k.mir,
+                   k.s.park};
     for (void *p : dev)
       if (p) (void)hipFree(p);
     zc_free(k.h_outs);
@@ -317,6 +341,7 @@ int finish(cog_env *e, bool refresh_host, cog_sampler *smp = nullptr) {
     if (host && k.zc) {
       const SamplerShard *q = smp ? &smp->sh[j] : nullptr;
       uint8_t *h_act = q ? const_cast<uint8_t *>(zc_device(smp->h_actions + q->first, q->n * COG_ACTION_BYTES)) : nullptr;
+      if (h_act && !zc_same_on(k.device, smp->h_actions + q->first)) h_act = nullptr;   // this GPU's mapping differs
       if (q && q->n && !h_act)
         HIPCHK(hipMemcpyAsync(smp->h_actions + q->first, q->d_actions, q->n * COG_ACTION_BYTES, hipMemcpyDeviceToHost,
                               k.stream));
@@ -445,7 +470,8 @@ int env_shard_init(EnvShard &k, uint32_t default_seed, uint32_t *err_word) {
       (rc = dmalloc(&s.priv, n * sizeof(cog::EnvPriv))) || (rc = dmalloc(&s.grid, n * (size_t)cog::kGridBytes)) ||
       (rc = dmalloc(&s.cgrid, n * (size_t)COG_CELLS)) || (rc = dmalloc(&s.heads, n * 5 * sizeof(uint4))) ||
       (rc = dmalloc(&s.gen, n * sizeof(cog::GenScratch))) || (rc = dmalloc(&s.dirty, n * sizeof(uint32_t))) ||
-      (rc = dmalloc(&k.d_actions, n * COG_ACTION_BYTES)) || (rc = zc_alloc(&k.h_outs, L.alloc)))
+      (rc = dmalloc(&k.d_actions, n * COG_ACTION_BYTES)) || (rc = dmalloc(&s.park, n * sizeof(uint32_t))) ||
+      (rc = zc_alloc(&k.h_outs, L.alloc)))
     return rc;
   std::memset(k.h_outs, 0, L.alloc);
   s.n = n;
@@ -466,6 +492,7 @@ int env_shard_init(EnvShard &k, uint32_t default_seed, uint32_t *err_word) {
                                        {k.d_actions, n * COG_ACTION_BYTES}};
   for (auto &zz : z)
     if (zz.b) HIPCHK(hipMemsetAsync(zz.p, 0, zz.b, k.stream));
+  if (n) HIPCHK(hipMemsetAsync(s.park, 0xff, n * sizeof(uint32_t), k.stream));   // no env parked
   if (cog::launch_init(s, nullptr, default_seed, k.stream))
     return fail(COG_ERR_HIP, std::string("env init kernel failed: ") + hipGetErrorString(hipGetLastError()));
   return COG_OK;
@@ -624,7 +651,7 @@ int cog_env_step(cog_env *env, const cog_action_t *actions, size_t n) {
     if (!k.n) continue;
     DeviceGuard g(k.device);
     const uint8_t *da = zc_device(actions + k.first, k.n * COG_ACTION_BYTES);   // read in place when pinned
-    if (!da) {
+    if (!da || !zc_same_on(k.device, actions + k.first)) {                      // (and mapped alike on this GPU)
       HIPCHK(hipMemcpyAsync(k.d_actions, actions + k.first, k.n * COG_ACTION_BYTES, hipMemcpyHostToDevice, k.stream));
       da = k.d_actions;
     }
@@ -790,7 +817,7 @@ int cog_time_copy(int device, size_t bytes, int iters, double *gb_per_s) {
               hipEventCreate(&e1) != hipSuccess || hipMemsetAsync(a, 1, bytes, st) != hipSuccess))
     rc = fail(COG_ERR_HIP, "copy setup");
   double best = 0.0;
-  for (int v = 0; v < 4 && !rc; v++) {                    // the fastest of the four variants
+  for (int v = 0; v < 8 && !rc; v++) {                    // the fastest of the eight variants
     if (cog::launch_copy_peak(a, b, bytes, st, v)) rc = fail(COG_ERR_HIP, "copy launch failed");   // warm-up
     if (rc) break;
     (void)hipEventRecord(e0, st);

@@ -103,6 +103,8 @@ struct DevState {
   uint32_t autoreset;                // 1: vec_cog_env (reset a finished env in the same call,
                                      // vec_environment.h:56-59); 0: cog_env (stays done)
   unsigned long long *stamps;        // diagnostic builds (COG_STAMPS) only: per-wave phase clocks
+  uint32_t *park;                    // [n] rollout park codes: the step at which an env's episode
+                                     // ended inside a launch (~0u: none), read by the fix-up kernel
 };
 
 struct ResetParams {
@@ -132,7 +134,8 @@ int launch_sample_step(const DevState &s, int mask_source, uint32_t *d_rng, uint
 int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions,
                    void *stream);                    // persistent K-step runner loop
 int launch_seed_sampler(size_t n, uint64_t seed, size_t first, uint32_t *d_rng, void *stream);
-// variant bit 0: non-temporal loads/stores; bit 1: 32 waves per CU instead of 8; bytes: a multiple of 16
+// variant bit 0: non-temporal loads/stores; bit 1: 32 waves per CU instead of 8 (grid stride);
+// bit 2: one pass, 32 KiB per workgroup (bit 1 ignored); bytes: a multiple of 16
 int launch_copy_peak(const void *src, void *dst, size_t bytes, void *stream, int variant);
 
 }  // namespace cog

@@ -22,6 +22,7 @@
 //   k_sync_heads     mask bit-vectors of every env from its byte records (init / reset)
 #include <hip/hip_runtime.h>
 #include <cstdlib>
+#include <cstring>
 
 #include "cog_engine.h"
 #include "cog_tables.h"
@@ -1217,10 +1218,12 @@ __global__ void k_init(DevState s, uint32_t default_seed) {
   }
 }
 
-__global__ void k_reset(DevState s, ResetParams p) {     // blocks of one wave (64 envs)
-  const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = i0 < s.n;
-  const size_t i = live ? i0 : 0;
+// blocks of one wave; lanes 0 .. epw - 1 own envs, the others only help the wave's cooperative
+// map generation (which runs one env at a time): a small batch spreads over many waves
+__global__ void k_reset(DevState s, ResetParams p, int epw) {
+  const size_t i0 = (size_t)blockIdx.x * epw + threadIdx.x;
+  const bool live = (int)threadIdx.x < epw && i0 < s.n;
+  const size_t i = live ? i0 : (size_t)blockIdx.x * epw;
   Ctx e = make_ctx(s, i);
   EnvPriv *pv = e.pv;
   if (live) {
@@ -2565,6 +2568,7 @@ DEV DevState wave_view(const DevState &s, size_t base) {
   v.cgrid += base * COG_CELLS;
   v.heads += 5 * base;
   v.gen += base;
+  v.park += base;
   v.first += base;
   v.n = s.n > base ? s.n - base : 0;
   return v;
@@ -2874,6 +2878,352 @@ __global__ void __launch_bounds__(128) k_env_rollout_pipe(DevState s, int steps,
 #endif
 }
 
+// ------------------------------------------------------------------------------------------
+// Duo rollout (round 3): two waves per 64-env workgroup -- a stepping wave and a storing wave --
+// sized so that FOUR workgroups share a CU (32,000 B of LDS each, <= 256 VGPRs + AGPRs per
+// work-item), i.e. two waves per SIMD at 65,536 envs.  A lone wave issues at most one
+// instruction per quad-cycle; the SIMD's VALU takes one per two cycles, so the storing wave of
+// one workgroup runs beside the stepping wave of another on the same SIMD, and the stepping wave
+// runs only the game logic.
+//
+// Ownership.  The stepping wave keeps the env in registers (RegEnv, across steps: no per-step
+// image repacking) and every player's counters, neighbourhood cache and stored-mask bits in LDS
+// (`pl`, `cells`, `heads`).  The storing wave keeps every player's DeckObs as last stored
+// (DeckImage, registers) and the "before" images the store phase compares with: the shared
+// block (phase, resources, shop), the selected-mask bits and each player's stored-mask bits.
+// Per step the stepping wave hands over only after-values through a single-buffered LDS ring
+// (`ring`, 14 granules per env), and the storing wave hands back the deck of the player who
+// acts after a turn change (`slot`: the next player's deck as of the step's start -- only the
+// acting player's deck changes within a step).
+//
+// Per step t, two barriers (both waves execute them):
+//   stepping wave: step t on registers; pl/cells/heads of the acting player to LDS;
+//                  X_t; record t to the ring; on a turn change the next player's records from
+//                  LDS and its deck from the slot; Y_t
+//   storing wave:  (X_0 after its prologue) Y_t; record t from the ring into registers; update
+//                  its images; the slot for step t + 1; X_{t+1}; the stores of record t
+// The storing wave reaches X long before the stepping wave ends its step, and the stepping wave
+// reaches Y long after the storing wave's stores were issued, so neither barrier stalls the
+// stepping wave beyond its own issue.
+//
+// Episode ends (and envs that start a launch done) park as in k_env_rollout's lean pass: the
+// lane stores its private state, records its park code in DevState::park and leaves the loop;
+// k_env_fixup, launched right after on the same stream, completes them.  The fix-up's register
+// appetite (map generation, the full step) therefore does not cap this kernel's occupancy.
+constexpr int kRingG = 7, kSlotG = 7;
+struct DuoLds {
+  uint4 pl[4][64];                    // [player][lane]: PlayerPriv (packed)
+  uint2 cells[4][64];                 // neighbourhood caches
+  uint4 heads[4][64];                 // stored-mask bits (MBits + pad)
+  uint4 ring[kRingG][64];             // step record, stepping wave -> storing wave
+  uint4 deckr[2][7][64];              // the record's DeckObs, double-buffered (written before X)
+  uint4 slot[kSlotG][64];             // next player's DeckObs, storing wave -> stepping wave
+  UidEntry tab[kUidTab];
+};
+static_assert(sizeof(DuoLds) <= 40960, "four duo workgroups per CU");
+// step record t: deckr[t & 1] = the acting player's DeckObs after the step, and ring granules
+//   0-2   ObsData 16128..16175 (phase, resources, shop) after the step
+//   3     selected-mask bits; .w = meta (below)
+//   4     the acting player's stored-mask bits; .w = action bytes 0..3
+//   5     the next player's stored-mask bits; .w = action byte 4
+//   6     EnvPriv granule 2 (map bounds + locations), read when the acting player moved
+// meta: bit 0 valid, 1 moved, 2-3 ag, 4-5 na, 6-7 na1 (the player after the next step's
+// acting player), 8-15 Info steps byte of ag, 16 the episode ended (parked: dones / agent are
+// left to the fix-up), 24-31 agent after the step
+constexpr uint32_t kMetaValid = 1u, kMetaMoved = 2u, kMetaEnded = 1u << 16;
+
+DEV uint32_t next_player(uint32_t a, uint32_t np) { return a + 1u >= np ? 0u : a + 1u; }
+
+// every private record of env i from the stepping wave (registers + the wave's LDS)
+DEV void duo_store_private_all(const DevState &s, size_t i, const RegEnv &R, const DuoLds &D, int l) {
+  uint4 *pw = reinterpret_cast<uint4 *>(s.priv + i);
+  pw[0] = make_uint4(R.rng, R.seed, R.max_steps, R.turn_counter);
+  pw[1] = make_uint4(R.g1x, R.g1y, R.in_market, R.flags);
+  reinterpret_cast<uint32_t *>(pw + 3)[0] = R.info_steps;
+  s.heads[5 * i] = mbits_u4(bits_of(R.sel));
+#pragma unroll
+  for (int p = 0; p < 4; p++) {
+    pw[4 + p] = D.pl[p][l];
+    reinterpret_cast<uint2 *>(pw + 8)[p] = D.cells[p][l];
+    s.heads[5 * i + 1 + p] = D.heads[p][l];
+  }
+}
+
+template <int SRC>
+DEV void duo_stepper(DuoLds &D, const DevState &s_glob, int steps, uint32_t *__restrict__ rngs_glob) {
+  const int l = threadIdx.x;
+  const size_t wbase = (size_t)blockIdx.x * 64;
+  const DevState s = wave_view(s_glob, wbase);
+  const size_t i = (size_t)l;
+  const int ne = (int)min((size_t)64, s_glob.n - wbase);
+  uint32_t *__restrict__ rngs = rngs_glob + wbase;
+  bool live = l < ne;
+  uint32_t park = kParkNone, srng = 0;
+  RegEnv R;
+  int ag = 0, na = 0;
+  if (live) {
+    Snap S;
+    load_env(s, i, S);
+    regs_env(R, S);
+    const uint4 *pv4 = reinterpret_cast<const uint4 *>(s.priv + i);
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+      D.pl[p][l] = pv4[4 + p];
+      D.cells[p][l] = reinterpret_cast<const uint2 *>(pv4 + 8)[p];
+      D.heads[p][l] = s.heads[5 * i + 1 + p];
+    }
+    srng = rngs[i];
+    ag = (int)R.agent();
+    na = (int)next_player((uint32_t)ag, R.n_players());
+    const uint4 *dk = reinterpret_cast<const uint4 *>(deck_ptr(s, i, ag));
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+      const uint4 v = dk[k];
+      R.d[4 * k] = v.x; R.d[4 * k + 1] = v.y; R.d[4 * k + 2] = v.z; R.d[4 * k + 3] = v.w;
+    }
+    R.P = unpack_player(D.pl[ag][l]);
+    R.na_active = (D.pl[na][l].y >> 16) & 0xffu;
+    R.cells_a = D.cells[ag][l];
+    R.cells_n = D.cells[na][l];
+    R.sta = heads_of(mbits_of(D.heads[ag][l]));
+    R.stn = heads_of(mbits_of(D.heads[na][l]));
+  }
+  R.tab = D.tab;
+  // every load above completes before the loop (no per-iteration vmcnt wait covers them)
+  __builtin_amdgcn_s_waitcnt(0);
+  PH_DECL;
+  for (int t = 0; t < steps; t++) {
+    bool ended = false, finish = false;
+    uint8_t act[5];
+    if (live) {
+      step_action<SRC>(R, nullptr, i, srng, act);
+      const bool was_done = R.done() != 0u;
+      finish = !was_done && step_regs(R, act, s, i, na PH_PASS);
+      if (finish) R.set_done(1u);
+      ended = was_done || finish;
+      PH(0);
+      D.pl[ag][l] = pack_player(R.P);
+      D.cells[ag][l] = R.cells_a;
+      D.heads[ag][l] = mbits_u4(bits_of(R.sta));
+      if (na != ag) D.heads[na][l] = mbits_u4(bits_of(R.stn));
+#pragma unroll
+      for (int k = 0; k < 7; k++)                          // (buffer t & 1: record t - 2's, taken)
+        D.deckr[t & 1][k][l] = make_uint4(R.d[4 * k], R.d[4 * k + 1], R.d[4 * k + 2], R.d[4 * k + 3]);
+      PH(1);
+    }
+    __syncthreads();                                       // X_t: record t - 1 taken, slot written
+    PH(2);
+    if (live) {
+      const int ag1 = (int)R.agent();
+      const int na1 = (int)next_player((uint32_t)ag1, R.n_players());
+      const MBits bs = bits_of(R.sel), ba = bits_of(R.sta), bn = bits_of(R.stn);
+      const uint32_t info = (R.info_steps >> (8 * ag)) & 0xffu;
+      const uint32_t meta = kMetaValid | (R.moved ? kMetaMoved : 0u) | (uint32_t)ag << 2 | (uint32_t)na << 4 |
+                            (uint32_t)na1 << 6 | info << 8 | (ended ? kMetaEnded : 0u) | (uint32_t)ag1 << 24;
+#pragma unroll
+      for (int k = 0; k < 3; k++) D.ring[k][l] = make_uint4(R.sh[4 * k], R.sh[4 * k + 1], R.sh[4 * k + 2], R.sh[4 * k + 3]);
+      D.ring[3][l] = make_uint4(bs.w0, bs.w1, bs.w2, meta);
+      D.ring[4][l] = make_uint4(ba.w0, ba.w1, ba.w2,
+                                (uint32_t)act[0] | (uint32_t)act[1] << 8 | (uint32_t)act[2] << 16 | (uint32_t)act[3] << 24);
+      D.ring[5][l] = make_uint4(bn.w0, bn.w1, bn.w2, (uint32_t)act[4]);
+      D.ring[6][l] = R.g2;
+      R.moved = false;
+      if (ag1 != ag) {                                     // turn change: ag1 == na acts next
+#pragma unroll
+        for (int k = 0; k < 7; k++) {
+          const uint4 v = D.slot[k][l];
+          R.d[4 * k] = v.x; R.d[4 * k + 1] = v.y; R.d[4 * k + 2] = v.z; R.d[4 * k + 3] = v.w;
+        }
+        R.P = unpack_player(D.pl[ag1][l]);
+        R.cells_a = R.cells_n;
+        R.sta = R.stn;
+        R.stn = heads_of(mbits_of(D.heads[na1][l]));
+        R.cells_n = D.cells[na1][l];
+        R.na_active = (D.pl[na1][l].y >> 16) & 0xffu;
+      }
+      if (ended) {                                         // hand the env to k_env_fixup
+        duo_store_private_all(s, i, R, D, l);
+        rngs[i] = srng;
+        park = (uint32_t)t | (finish ? kParkFinish : 0u);
+        live = false;
+      }
+      ag = ag1;
+      na = na1;
+    } else {
+      D.ring[3][l] = make_uint4(0u, 0u, 0u, 0u);           // no record
+    }
+    PH(3);
+    __syncthreads();                                       // Y_t: record t in the ring
+    PH(4);
+  }
+  __syncthreads();                                         // X_steps
+  PH_FLUSH(s_glob);
+  if (live) {                                              // env-level private state back to HBM
+    uint4 *pw = reinterpret_cast<uint4 *>(s.priv + i);
+    pw[0] = make_uint4(R.rng, R.seed, R.max_steps, R.turn_counter);
+    pw[1] = make_uint4(R.g1x, R.g1y, R.in_market, R.flags);
+    reinterpret_cast<uint32_t *>(pw + 3)[0] = R.info_steps;
+    s.heads[5 * i] = mbits_u4(bits_of(R.sel));
+    rngs[i] = srng;
+  }
+  if (l < ne) s.park[i] = park;
+  lds_store_wave<DuoLds, 64>(D, s, 0, ne);                 // every player's records (cooperative)
+}
+
+DEV uint4 sel4_of(const DeckImage &I, int p, int k) {      // I.d[p][k] for a lane-varying p
+  uint4 v = I.d[3][k];
+#pragma unroll
+  for (int q = 2; q >= 0; q--) v = sel4(p == q, I.d[q][k], v);
+  return v;
+}
+DEV MBits selm(const MBits b[4], int p) {
+  MBits v = b[3];
+#pragma unroll
+  for (int q = 2; q >= 0; q--) {
+    v.w0 = p == q ? b[q].w0 : v.w0;
+    v.w1 = p == q ? b[q].w1 : v.w1;
+    v.w2 = p == q ? b[q].w2 : v.w2;
+  }
+  return v;
+}
+DEV void setm(MBits b[4], int p, const MBits &v) {
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    b[q].w0 = p == q ? v.w0 : b[q].w0;
+    b[q].w1 = p == q ? v.w1 : b[q].w1;
+    b[q].w2 = p == q ? v.w2 : b[q].w2;
+  }
+}
+
+DEV void duo_storer(DuoLds &D, const DevState &s_glob, int steps, uint8_t *__restrict__ actions_glob) {
+  const int l = (int)threadIdx.x - 64;
+  const size_t wbase = (size_t)blockIdx.x * 64;
+  const DevState s = wave_view(s_glob, wbase);
+  const size_t i = (size_t)l;
+  const bool live = wbase + (size_t)l < s_glob.n;
+  uint8_t *__restrict__ av = actions_glob + wbase * COG_ACTION_BYTES;
+  DeckImage I;
+  uint4 shb[3];
+  MBits selb = {0u, 0u, 0u}, stb[4];
+  uint32_t out = ~0u;                                      // dones[i] | agent_selection[i] << 8 as stored
+  if (live) {
+    deck_image_load(I, s, i);
+    const uint4 *sh4 = reinterpret_cast<const uint4 *>(s.obs + i * COG_OBS_BYTES + COG_OBS_PHASE);
+#pragma unroll
+    for (int k = 0; k < 3; k++) shb[k] = sh4[k];
+    selb = mbits_of(s.heads[5 * i]);
+#pragma unroll
+    for (int p = 0; p < 4; p++) stb[p] = mbits_of(s.heads[5 * i + 1 + p]);
+    const uint4 g1 = reinterpret_cast<const uint4 *>(s.priv + i)[1];
+    const int na0 = (int)next_player(g1.y & 0xffu, g1.x & 0xffu);
+#pragma unroll
+    for (int k = 0; k < 7; k++) D.slot[k][l] = sel4_of(I, na0, k);
+  }
+  __syncthreads();                                         // X_0
+  PH_DECL;
+  for (int t = 0; t < steps; t++) {
+    __syncthreads();                                       // Y_t
+    PH(5);
+    uint4 g[kRingG], dk[7];
+#pragma unroll
+    for (int k = 0; k < kRingG; k++) g[k] = D.ring[k][l];
+#pragma unroll
+    for (int k = 0; k < 7; k++) dk[k] = D.deckr[t & 1][k][l];
+    const uint32_t meta = g[3].w;
+    const bool rec = live && (meta & kMetaValid);
+    const int ag = (int)((meta >> 2) & 3u), na = (int)((meta >> 4) & 3u), na1 = (int)((meta >> 6) & 3u);
+    if (rec) {
+      uint32_t dm = 0;                                     // deck granules that changed
+#pragma unroll
+      for (int k = 0; k < 7; k++) {
+        if (ne4(dk[k], sel4_of(I, ag, k))) dm |= 1u << k;
+#pragma unroll
+        for (int p = 0; p < 4; p++) I.d[p][k] = sel4(ag == p, dk[k], I.d[p][k]);
+      }
+#pragma unroll
+      for (int k = 0; k < 7; k++) D.slot[k][l] = sel4_of(I, na1, k);
+      PH(6);
+      uint8_t *ob = s.obs + i * COG_OBS_BYTES;
+      s.info[i * COG_INFO_BYTES + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag] = (uint8_t)(meta >> 8);
+      if (meta & kMetaMoved) reinterpret_cast<uint4 *>(s.priv + i)[2] = g[6];
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        if (ne4(g[k], shb[k])) reinterpret_cast<uint4 *>(ob + COG_OBS_PHASE)[k] = g[k];
+        shb[k] = g[k];
+      }
+      uint8_t *deck = deck_ptr(s, i, ag);
+#pragma unroll
+      for (int k = 0; k < 7; k++)
+        if ((dm >> k) & 1u) reinterpret_cast<uint4 *>(deck)[k] = dk[k];
+      const MBits bs{g[3].x, g[3].y, g[3].z}, ba{g[4].x, g[4].y, g[4].z};
+      store_mask_record(reinterpret_cast<uint4 *>(s.sel + i * COG_MASK_BYTES), bs, mask_diff_granules(bs, selb));
+      selb = bs;
+      store_mask_record(reinterpret_cast<uint4 *>(deck + COG_PD_MASK), ba, mask_diff_granules(ba, selm(stb, ag)));
+      setm(stb, ag, ba);
+      if (na != ag) {
+        const MBits bn{g[5].x, g[5].y, g[5].z};
+        store_mask_record(reinterpret_cast<uint4 *>(deck_ptr(s, i, na) + COG_PD_MASK), bn,
+                          mask_diff_granules(bn, selm(stb, na)));
+        setm(stb, na, bn);
+      }
+      reinterpret_cast<uint2 *>(av + i * COG_ACTION_BYTES)[0] = make_uint2(g[4].w, g[5].w);
+      if (!(meta & kMetaEnded)) {                          // dones[i] = 0, agent_selection[i]
+        const uint32_t agent = meta >> 24;                 // (an ended episode: k_env_fixup)
+        if (out & 0xffu) s.done[i] = 0;
+        if (((out >> 8) & 0xffu) != agent) s.agent[i] = (uint8_t)agent;
+        out = agent << 8;
+      }
+    }
+    PH(13);
+    __syncthreads();                                       // X_{t+1}
+    PH(7);
+  }
+  PH_FLUSH(s_glob);
+}
+
+template <int SRC>
+__global__ void __launch_bounds__(128) k_env_rollout_duo(DevState s, int steps, uint32_t *__restrict__ rngs,
+                                                         uint8_t *__restrict__ actions_out) {
+  __shared__ DuoLds D;
+  const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform
+  uid_tab_fill(D.tab);
+  if (role == 0) {
+#ifndef DUO_NOPRIO                                         // (diagnostic A/B builds only)
+    __builtin_amdgcn_s_setprio(3);                         // the stepping wave wins VALU issue on
+#endif
+    duo_stepper<SRC>(D, s, steps, rngs);                   // a SIMD it shares with a storing wave
+  } else {
+    duo_storer(D, s, steps, actions_out);
+  }
+}
+
+// The episode ends k_env_rollout_duo parked: a wave with a parked lane runs k_env_rollout's
+// fix-up pass for exactly those lanes (finish_episode, dones, auto-reset with the wave's map
+// generation and encode, then the env's remaining steps with the full step); a wave with none
+// returns after one load.  Same stream, right after the rollout launch: nothing reads the envs
+// in between.
+template <int SRC>
+__global__ void __launch_bounds__(64) k_env_fixup(DevState s, int steps, uint32_t *__restrict__ rngs,
+                                                  uint8_t *__restrict__ actions_out) {
+  __shared__ LaneLds<64> L;
+  const size_t base = (size_t)blockIdx.x * 64;
+  const size_t i0 = base + threadIdx.x;
+  const uint32_t park = i0 < s.n ? s.park[i0] : kParkNone;
+  if (!__builtin_amdgcn_ballot_w64(park != kParkNone)) return;   // (wave-uniform)
+  uid_tab_fill(L.tab);
+  rollout_pass<SRC, true, 64>(L, s, steps, rngs, actions_out, park);
+  if (park != kParkNone) {                                 // the parked envs' player records
+    const int l = (int)threadIdx.x;
+    uint4 *pw = reinterpret_cast<uint4 *>(s.priv + i0);
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+      pw[4 + p] = L.pl[p][l];
+      reinterpret_cast<uint2 *>(pw + 8)[p] = L.cells[p][l];
+      s.heads[5 * i0 + 1 + p] = L.heads[p][l];
+    }
+    s.park[i0] = kParkNone;
+  }
+}
 
 // masks may be device memory or pinned host memory (zero-copy); h_actions (may be null) is the
 // host view of the actions, written straight over PCIe beside the device copy
@@ -2968,6 +3318,21 @@ __global__ void __launch_bounds__(256) k_copy_peak(const u32x4_t *__restrict__ s
   }
   for (; i < n16; i += stride) cp_st<NT>(cp_ld<NT>(src + i), dst + i);
 }
+// one pass, no grid stride: a workgroup copies one contiguous 32 KiB block (8 granules in flight
+// per work-item, all loads issued before the first store); a grid of n16 / 2048 workgroups
+template <bool NT>
+__global__ void __launch_bounds__(256) k_copy_block(const u32x4_t *__restrict__ src, u32x4_t *__restrict__ dst, size_t n16) {
+  const size_t base = (size_t)blockIdx.x * 2048 + threadIdx.x;
+  if (base + 7 * 256 < n16) {
+    u32x4_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = cp_ld<NT>(src + base + k * 256);
+#pragma unroll
+    for (int k = 0; k < 8; k++) cp_st<NT>(v[k], dst + base + k * 256);
+  } else {
+    for (size_t i = base; i < n16; i += 256) cp_st<NT>(cp_ld<NT>(src + i), dst + i);
+  }
+}
 
 // ------------------------------------------------------------------------------------------
 // host launchers
@@ -2982,7 +3347,14 @@ int launch_init(const DevState &s, const uint32_t *, uint32_t default_seed, void
 }
 int launch_reset(const DevState &s, const ResetParams &p, void *stream) {
   if (!s.n) return 0;
-  hipLaunchKernelGGL(k_reset, dim3(blocks_for(s.n, 64)), dim3(64), 0, (hipStream_t)stream, s, p);
+  // envs per wave: enough waves to keep every SIMD generating (about 4,096 waves), at most 64
+  static const int epw_env = [] {
+    const char *e = getenv("COG_RESET_EPW");
+    return e ? atoi(e) : 0;
+  }();
+  const size_t auto_epw = (s.n + 4095) / 4096;
+  const int epw = epw_env > 0 ? (epw_env < 64 ? epw_env : 64) : (int)(auto_epw < 1 ? 1 : auto_epw > 64 ? 64 : auto_epw);
+  hipLaunchKernelGGL(k_reset, dim3(blocks_for(s.n, (unsigned)epw)), dim3(64), 0, (hipStream_t)stream, s, p, epw);
   hipLaunchKernelGGL(k_sync_heads, dim3(blocks_for(s.n, 256)), dim3(256), 0, (hipStream_t)stream, s);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -3029,21 +3401,44 @@ static void rollout_launch(const DevState &s, int mask_source, int steps, uint32
   else
     hipLaunchKernelGGL((k_env_rollout<MASK_SELECTED, NL>), g, b, 0, st, s, steps, d_rng, d_actions);
 }
-// shards up to this size take the two-wave rollout; $COG_ROLLOUT_PIPE_MAX overrides it (0: never)
-static size_t pipe_max_envs() {
-  static const size_t v = [] {
-    const char *e = getenv("COG_ROLLOUT_PIPE_MAX");
-    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)32768;
+// Which rollout kernels run a shard of n envs (measured on MI355X, device us/step in 1,000-step
+// launches, profiles/r03_rollout_kinds.txt):
+//   n <= 16,384  duo   (k_env_rollout_duo + k_env_fixup: 2.47-2.49 against pipe 2.65-2.68)
+//   n <= 32,768  pipe  (k_env_rollout_pipe: 2.75-2.76 against duo 2.96)
+//   larger       wave  (k_env_rollout: 3.91-3.96 against duo 4.0-4.7)
+// Above 16,384 envs the chip's shader clock drops (2.34 -> 2.08 GHz measured by s_memtime at the
+// same cycles per step), and the duo's storing wave costs more work per env-step than its
+// hand-off saves, so the leaner kernels win there.  $COG_ROLLOUT = duo | pipe | wave forces one.
+enum RolloutKind : int { RK_AUTO = -1, RK_DUO = 0, RK_WAVE = 1, RK_PIPE = 2 };
+static int rollout_kind(size_t n) {
+  static const int forced = [] {
+    const char *e = getenv("COG_ROLLOUT");
+    if (!e || !*e || !strcmp(e, "auto")) return (int)RK_AUTO;
+    return !strcmp(e, "duo") ? (int)RK_DUO : !strcmp(e, "wave") ? (int)RK_WAVE : (int)RK_PIPE;
   }();
-  return v;
+  if (forced != RK_AUTO) return forced;
+  return n <= 16384 ? RK_DUO : n <= 32768 ? RK_PIPE : RK_WAVE;
 }
 int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions, void *stream) {
   if (!s.n || steps <= 0) return 0;
+  const int kind = rollout_kind(s.n);
+  if (kind == RK_DUO) {
+    const hipStream_t st = (hipStream_t)stream;
+    const dim3 g(blocks_for(s.n, 64));
+    if (mask_source == MASK_STORED) {
+      hipLaunchKernelGGL((k_env_rollout_duo<MASK_STORED>), g, dim3(128), 0, st, s, steps, d_rng, d_actions);
+      hipLaunchKernelGGL((k_env_fixup<MASK_STORED>), g, dim3(64), 0, st, s, steps, d_rng, d_actions);
+    } else {
+      hipLaunchKernelGGL((k_env_rollout_duo<MASK_SELECTED>), g, dim3(128), 0, st, s, steps, d_rng, d_actions);
+      hipLaunchKernelGGL((k_env_fixup<MASK_SELECTED>), g, dim3(64), 0, st, s, steps, d_rng, d_actions);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   // one 64-env wave per workgroup: 32-env workgroups measured 7.3 us/step against 3.8 at 65,536
   // envs (round 2).  The kernel's register allocation (about 490 VGPRs + AGPRs per work-item)
   // admits one wave per SIMD, so 2,048 half-empty waves ran in two rounds on 1,024 SIMDs
   const hipStream_t st = (hipStream_t)stream;
-  if (s.n <= pipe_max_envs()) {                            // SIMDs to spare: the two-wave form
+  if (kind == RK_PIPE) {                                   // SIMDs to spare: the two-wave form
     const dim3 g(blocks_for(s.n, 64)), b(128);
     if (mask_source == MASK_STORED)
       hipLaunchKernelGGL((k_env_rollout_pipe<MASK_STORED>), g, b, 0, st, s, steps, d_rng, d_actions);
@@ -3068,9 +3463,16 @@ size_t publish_mirror_bytes(size_t n, size_t outs_bytes) { return n * kTailG * 1
 int launch_copy_peak(const void *src, void *dst, size_t bytes, void *stream, int variant) {
   const u32x4_t *a = static_cast<const u32x4_t *>(src);
   u32x4_t *b = static_cast<u32x4_t *>(dst);
-  const dim3 g(variant & 2 ? 8192 : 2048), t(256);   // 8 or 32 waves per CU
-  if (variant & 1) hipLaunchKernelGGL(k_copy_peak<true>, g, t, 0, (hipStream_t)stream, a, b, bytes / 16);
-  else hipLaunchKernelGGL(k_copy_peak<false>, g, t, 0, (hipStream_t)stream, a, b, bytes / 16);
+  const size_t n16 = bytes / 16;
+  if (variant & 4) {                                  // one pass, 32 KiB per workgroup
+    const dim3 g(blocks_for(n16, 2048)), t(256);
+    if (variant & 1) hipLaunchKernelGGL(k_copy_block<true>, g, t, 0, (hipStream_t)stream, a, b, n16);
+    else hipLaunchKernelGGL(k_copy_block<false>, g, t, 0, (hipStream_t)stream, a, b, n16);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+  const dim3 g(variant & 2 ? 8192 : 2048), t(256);   // grid stride: 8 or 32 waves per CU
+  if (variant & 1) hipLaunchKernelGGL(k_copy_peak<true>, g, t, 0, (hipStream_t)stream, a, b, n16);
+  else hipLaunchKernelGGL(k_copy_peak<false>, g, t, 0, (hipStream_t)stream, a, b, n16);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_seed_sampler(size_t n, uint64_t seed, size_t first, uint32_t *d_rng, void *stream) {

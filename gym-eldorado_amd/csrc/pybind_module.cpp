@@ -81,11 +81,11 @@ static void check(int rc) {
 }
 
 // Devices of a new handle (reference: one object owns every env, vectorized.h:185-214).
-//   device=None: COG_DEVICES ("0,2,..."), else LOCAL_RANK (one process per GPU under torchrun),
-//                else COG_DEVICE, else every visible GPU with at least kMinShard envs per shard
-//                (a small batch stays on one GPU);
+//   device=None: COG_DEVICES ("0,2,...": opt-in sharding over several GPUs), else COG_DEVICE
+//                (pins the GPU, e.g. several ranks on one GPU), else LOCAL_RANK (one process per
+//                GPU under torchrun), else GPU 0.  A handle never spans GPUs unless asked to, so
+//                device views (device_tensors, step_device, sampler.dlpack) keep one shard.
 //   device=int:  that GPU;  device=[d0, d1, ...]: one contiguous shard per entry.
-constexpr size_t kMinShard = 8192;
 static std::vector<int> parse_list(const char *v) {
   std::vector<int> out;
   const char *p = v;
@@ -100,22 +100,17 @@ static std::vector<int> parse_list(const char *v) {
   if (out.empty()) throw py::value_error("empty device list");
   return out;
 }
-static std::vector<int> default_devices(size_t n) {
+static std::vector<int> default_devices() {
   const char *v = std::getenv("COG_DEVICES");
   if (v && *v) return parse_list(v);
-  const char *lr = std::getenv("LOCAL_RANK");
-  if (lr && *lr) return {std::atoi(lr)};
   const char *d = std::getenv("COG_DEVICE");
   if (d && *d) return {std::atoi(d)};
-  int cnt = 0;
-  if (cog_device_count(&cnt) != COG_OK || cnt <= 1) return {0};
-  const size_t k = std::min<size_t>((size_t)cnt, std::max<size_t>(1, n / kMinShard));
-  std::vector<int> out;
-  for (size_t j = 0; j < k; j++) out.push_back((int)j);
-  return out;
+  const char *lr = std::getenv("LOCAL_RANK");
+  if (lr && *lr) return {std::atoi(lr)};
+  return {0};
 }
-static std::vector<int> devices_of(const py::object &device, size_t n) {
-  if (device.is_none()) return default_devices(n);
+static std::vector<int> devices_of(const py::object &device, size_t) {
+  if (device.is_none()) return default_devices();
   if (py::isinstance<py::int_>(device)) return {device.cast<int>()};
   std::vector<int> out = device.cast<std::vector<int>>();
   if (out.empty()) throw py::value_error("device list is empty");
@@ -335,6 +330,8 @@ PYBIND11_MODULE(_city_of_gold, m) {
     check(cog_device_count(&n));
     return n;
   });
+  m.def("default_devices", []() { return default_devices(); },
+        "the GPUs a handle created with device=None uses (COG_DEVICES, else COG_DEVICE, else LOCAL_RANK, else 0)");
   m.def(
       "time_copy",
       [](int device, size_t bytes, int iters) {

@@ -869,6 +869,40 @@ int orc_reset(orc_vec *v, uint32_t seed, uint8_t n_players, uint8_t n_pieces, in
   return 0;
 }
 
+/* orc_reset over n_threads threads (envs are independent; each env's reset is the serial one) */
+typedef struct { orc_vec *v; uint32_t seed; uint8_t np, npc; int diff; uint32_t ms; size_t lo, hi; int rc; } reset_arg;
+static void *reset_worker(void *p) {
+  reset_arg *a = (reset_arg *)p;
+  for (size_t i = a->lo; i < a->hi; i++) {
+    oenv *e = &a->v->env[i];
+    e->n_players = a->np; e->n_pieces = a->npc; e->difficulty = (uint8_t)a->diff;
+    e->max_steps = a->ms;
+    e->seed = (uint32_t)(a->seed + (uint32_t)i);
+    e->rng = mr_seed(e->seed);
+    if (env_reset(e)) a->rc = -1;
+  }
+  return NULL;
+}
+int orc_reset_threaded(orc_vec *v, uint32_t seed, uint8_t n_players, uint8_t n_pieces, int difficulty,
+                       uint32_t max_steps, int n_threads) {
+  if (n_threads < 1) n_threads = 1;
+  pthread_t *th = (pthread_t *)calloc((size_t)n_threads, sizeof(pthread_t));
+  reset_arg *ra = (reset_arg *)calloc((size_t)n_threads, sizeof(reset_arg));
+  const size_t b = v->n / (size_t)n_threads;
+  int rc = 0;
+  for (int i = 0; i < n_threads; i++) {
+    ra[i] = (reset_arg){v, seed, n_players, n_pieces, difficulty, max_steps, (size_t)i * b,
+                        i < n_threads - 1 ? (size_t)(i + 1) * b : v->n, 0};
+    pthread_create(&th[i], NULL, reset_worker, &ra[i]);
+  }
+  for (int i = 0; i < n_threads; i++) {
+    pthread_join(th[i], NULL);
+    rc |= ra[i].rc;
+  }
+  free(th); free(ra);
+  return rc;
+}
+
 int orc_reset_default(orc_vec *v) {
   for (size_t i = 0; i < v->n; i++)
     if (env_reset(&v->env[i])) return -1;

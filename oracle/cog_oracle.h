@@ -41,6 +41,8 @@ size_t orc_num_envs(const orc_vec *v);
 int orc_reset(orc_vec *v, uint32_t seed, uint8_t n_players, uint8_t n_pieces,
               int difficulty, uint32_t max_steps);
 int orc_reset_default(orc_vec *v);
+int orc_reset_threaded(orc_vec *v, uint32_t seed, uint8_t n_players, uint8_t n_pieces,
+                       int difficulty, uint32_t max_steps, int n_threads);
 /* vec_cog_env::step: actions = n ActionData records (64 B stride) */
 int orc_step(orc_vec *v, const void *actions);
 /* step only envs [lo, hi) */

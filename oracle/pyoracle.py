@@ -96,6 +96,7 @@ class _Lib:
             lib.orc_destroy.argtypes = [vp]
             lib.orc_reset.argtypes = [vp, C.c_uint32, C.c_uint8, C.c_uint8, C.c_int, C.c_uint32]
             lib.orc_reset_default.argtypes = [vp]
+            lib.orc_reset_threaded.argtypes = [vp, C.c_uint32, C.c_uint8, C.c_uint8, C.c_int, C.c_uint32, C.c_int]
             lib.orc_step.argtypes = [vp, vp]
             lib.orc_step_range.argtypes = [vp, vp, sz, sz]
             for f in ("orc_obs", "orc_sel", "orc_rewards", "orc_dones", "orc_agent_sel", "orc_infos"):
@@ -168,6 +169,13 @@ class OracleVec:
         if self.lib.orc_reset(self.h, seed & 0xFFFFFFFF, n_players, n_pieces, int(difficulty), max_steps):
             raise RuntimeError("Failed to generate map in specified maximum number of attempts")
 
+    def reset_threaded(self, seed, n_players=4, n_pieces=3, difficulty=0, max_steps=100000, threads=None):
+        """reset() split over `threads` host threads (bit-identical: envs are independent)."""
+        threads = threads or host_threads()
+        if self.lib.orc_reset_threaded(self.h, seed & 0xFFFFFFFF, n_players, n_pieces, int(difficulty),
+                                       max_steps, threads):
+            raise RuntimeError("Failed to generate map in specified maximum number of attempts")
+
     def reset_default(self):
         if self.lib.orc_reset_default(self.h):
             raise RuntimeError("Failed to generate map in specified maximum number of attempts")
@@ -226,6 +234,17 @@ def ref_layout():
 
 def ref_available():
     return os.path.exists(REF_SO)
+
+
+def host_threads():
+    """Worker threads for oracle runs: this process's CPU share (OMP_NUM_THREADS caps it on the
+    GPU box, where os.cpu_count() reports the whole machine)."""
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except Exception:
+        allowed = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", allowed) or allowed)
+    return max(1, min(allowed, share))
 
 
 def run_threaded(vec: OracleVec, sampler: OracleSampler, steps: int, n_threads: int) -> float:

@@ -94,3 +94,26 @@ def test_no_gpu_fails_loudly(cg):
         cg.vec.get_vec_env(4)()
     with pytest.raises(RuntimeError):
         cg.vec.get_vec_sampler(4)(0)
+
+
+def test_default_device_order(cg, monkeypatch):
+    """device=None: COG_DEVICES, else COG_DEVICE, else LOCAL_RANK, else GPU 0 -- never an implicit
+    split over every visible GPU; bench.device_of follows the same order."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    for k in ("COG_DEVICES", "COG_DEVICE", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    dd = cg._city_of_gold.default_devices
+    assert dd() == [0]
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    assert dd() == [3]
+    d = type("D", (), {"local": 3})()
+    assert bench.device_of(d) == 3
+    monkeypatch.setenv("COG_DEVICE", "1")
+    assert dd() == [1] and bench.device_of(d) == 1
+    monkeypatch.setenv("COG_DEVICES", "0,2")
+    assert dd() == [0, 2]
+    monkeypatch.setenv("COG_DEVICES", "0,x")
+    with pytest.raises(ValueError):
+        dd()

@@ -1,0 +1,92 @@
+// Diagnostic only: the duo rollout (k_env_rollout_duo + k_env_fixup) on the bench workload.
+// Prints the device us/step of 1,000-step and 20-step launches per env count; built with
+// -DCOG_STAMPS it also prints the per-phase s_memtime ticks per step of the stepping and the
+// storing waves (median over waves).  Variants: -DDUO_* ablations in the engine source.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -mllvm -amdgpu-sched-strategy=max-ilp \
+//         -Iinclude -Igym-eldorado_amd/csrc [-DCOG_STAMPS] tools/duoprobe.cpp -o tools/duoprobe
+#include "../gym-eldorado_amd/csrc/cog_engine.hip"
+#include "../gym-eldorado_amd/csrc/cog_abi.cpp"
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+static double med(std::vector<double> v) {
+  std::sort(v.begin(), v.end());
+  return v[v.size() / 2];
+}
+
+int main(int argc, char **argv) {
+  const char *tag = argc > 1 ? argv[1] : "duo";
+  std::vector<size_t> sizes;
+  for (int a = 2; a < argc; a++) sizes.push_back(strtoul(argv[a], nullptr, 10));
+  if (sizes.empty()) sizes = {65536, 32768, 16384, 8192};
+  for (size_t n : sizes) {
+    cog_env *env;
+    cog_sampler *smp;
+    cog_runner *run;
+    if (cog_env_create(n, 0, &env) || cog_sampler_create(n, 12345, 0, &smp) ||
+        cog_env_reset(env, 12345, 4, 3, 2, 100000, 0) || cog_runner_create(env, smp, 1, COG_RUNNER_DEVICE_VIEWS, &run)) {
+      printf("setup failed: %s\n", cog_last_error());
+      return 1;
+    }
+    cog_runner_set_chunk(run, 1000);
+    cog_runner_rollout(run, 200);
+    cog_runner_sync(run);
+    hipStream_t st = env->sh[0].stream;
+    hipEvent_t a, b;
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return 1;
+    auto timed = [&](int k, int reps) {
+      std::vector<double> v;
+      cog_runner_set_chunk(run, k);
+      for (int r = 0; r < reps; r++) {
+        if (hipEventRecord(a, st) != hipSuccess) return -1.0;
+        cog_runner_rollout(run, k);
+        if (hipEventRecord(b, st) != hipSuccess || hipEventSynchronize(b) != hipSuccess) return -1.0;
+        float ms;
+        if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return -1.0;
+        v.push_back(ms * 1e3);
+      }
+      return med(v);
+    };
+    const double r1000 = timed(1000, 5), r20 = timed(20, 25);
+    printf("%s n=%6zu  %6.3f us/step (1000-step launches)  20-step launch %7.2f us (%5.3f us/step)\n", tag, n,
+           r1000 / 1000, r20, r20 / 20);
+    fflush(stdout);
+#ifdef COG_STAMPS
+    {
+      const size_t waves = 2 * ((n + 63) / 64);
+      constexpr int K = 16;
+      unsigned long long *d;
+      if (hipMalloc(&d, waves * K * sizeof(unsigned long long)) != hipSuccess) return 1;
+      if (hipMemset(d, 0, waves * K * sizeof(unsigned long long)) != hipSuccess) return 1;
+      env->sh[0].s.stamps = d;
+      const int chunk = 200;
+      cog_runner_set_chunk(run, chunk);
+      cog_runner_rollout(run, chunk);
+      cog_runner_sync(run);
+      env->sh[0].s.stamps = nullptr;
+      std::vector<unsigned long long> h(waves * K);
+      if (hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+      const char *pn[16] = {"S: step tail (done check)", "S: LDS player writes", "S: wait X", "S: ring write + turn change",
+                            "S: wait Y", "W: wait Y", "W: ring read, images, slot", "W: wait X",
+                            "S: sample + action branch", "S: mip + end_turn discard", "S: draw", "S: mask swap, sh, cells",
+                            "S: update_observation", "W: stores", "", ""};
+      double tot[2] = {0, 0};
+      for (int k = 0; k < 14; k++) {
+        const int role = pn[k][0] == 'S' ? 0 : 1;
+        std::vector<double> v;
+        for (size_t w = role; w < waves; w += 2) v.push_back((double)h[w * K + k] / chunk);
+        const double m = med(v);
+        tot[role] += m;
+        printf("  %-36s %8.0f\n", pn[k], m);
+      }
+      printf("  stepping wave sum %8.0f   storing wave sum %8.0f  (ticks per step)\n", tot[0], tot[1]);
+      (void)hipFree(d);
+    }
+#endif
+    cog_runner_destroy(run);
+    cog_sampler_destroy(smp);
+    cog_env_destroy(env);
+  }
+  return 0;
+}
