@@ -3143,6 +3143,7 @@ DEV void duo_storer(DuoLds &D, const DevState &s_glob, int steps, uint8_t *__res
 #pragma unroll
       for (int k = 0; k < 7; k++) D.slot[k][l] = sel4_of(I, na1, k);
       PH(6);
+#ifndef COG_ABLATE_DUOSTORES                               // diagnostic timing builds only
       uint8_t *ob = s.obs + i * COG_OBS_BYTES;
       s.info[i * COG_INFO_BYTES + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag] = (uint8_t)(meta >> 8);
       if (meta & kMetaMoved) reinterpret_cast<uint4 *>(s.priv + i)[2] = g[6];
@@ -3167,6 +3168,9 @@ DEV void duo_storer(DuoLds &D, const DevState &s_glob, int steps, uint8_t *__res
         setm(stb, na, bn);
       }
       reinterpret_cast<uint2 *>(av + i * COG_ACTION_BYTES)[0] = make_uint2(g[4].w, g[5].w);
+#else
+      asm volatile("" ::"v"(g[0].x ^ g[1].y ^ g[2].z ^ g[3].x ^ g[4].y ^ g[5].z ^ g[6].w ^ dm ^ dk[0].x ^ dk[6].w));
+#endif
       if (!(meta & kMetaEnded)) {                          // dones[i] = 0, agent_selection[i]
         const uint32_t agent = meta >> 24;                 // (an ended episode: k_env_fixup)
         if (out & 0xffu) s.done[i] = 0;
