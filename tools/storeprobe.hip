@@ -42,7 +42,7 @@ __global__ void __launch_bounds__(256) k_store(uint8_t *obs, size_t n, int steps
       const size_t e = e0 + (size_t)slice * (64 / LPE) + grp;
       // SPREAD: each granule of a step in its own 128-B line of the tail, the set of lines
       // shifting every 8 steps (a new acting player): a per-XCD footprint beyond the 4 MiB L2
-      const int g = SPREAD ? (((k * 3 + ((t >> 3) & 3) * 2) % 8) * 8 + (t & 1))
+      const int g = SPREAD ? (((k / LPE) * 3 + ((t >> 3) & 3) * 2) % 8) * 8 + (t & 1) * 4 + sub
                            : ((k / LPE) * LPE + sub) % 68;  // granule in the tail (68 x 16 B)
       st16<MODE>(reinterpret_cast<uint4 *>(obs + e * kObs + kTail + 16 * g), v);
       v.z += 1u;
@@ -62,20 +62,23 @@ int main(int argc, char **argv) {
   const dim3 grid((unsigned)((n / 64 + wpg - 1) / wpg)), blk(64 * wpg);
   if (argc > 3) {                                            // G granules per env-step, spread vs packed
     const int g = atoi(argv[3]);
-    for (int sp = 0; sp < 2; sp++) {
+    for (int sp = 0; sp < 4; sp++) {                       // packed, spread, spread 2 and 4 lanes per env
       float best = 1e30f;
       for (int r = 0; r < 3; r++) {
         if (hipEventRecord(a, 0) != hipSuccess) return 1;
-        if (sp) hipLaunchKernelGGL((k_store<1, 0, true>), grid, blk, 0, 0, obs, n, steps, g);
+        if (sp == 1) hipLaunchKernelGGL((k_store<1, 0, true>), grid, blk, 0, 0, obs, n, steps, g);
+        else if (sp == 2) hipLaunchKernelGGL((k_store<2, 0, true>), grid, blk, 0, 0, obs, n, steps, 2 * g);
+        else if (sp == 3) hipLaunchKernelGGL((k_store<4, 0, true>), grid, blk, 0, 0, obs, n, steps, 4 * g);
         else hipLaunchKernelGGL((k_store<1, 0, false>), grid, blk, 0, 0, obs, n, steps, g);
         if (hipEventRecord(b, 0) != hipSuccess || hipEventSynchronize(b) != hipSuccess) return 1;
         float ms;
         if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 1;
         best = ms < best ? ms : best;
       }
-      printf("n=%zu wpg=%d %s: %d scattered 16-B stores per env-step: %.3f us per step, %.0f G requests/s\n", n, wpg,
-             sp ? "spread (6 lines/env-step, footprint > L2)" : "packed (2 lines/env)", g, best * 1e3 / steps,
-             (double)n * g * steps / (best * 1e-3) / 1e9);
+      const char *what[4] = {"packed (2 lines/env), 16 B per line", "spread (footprint > L2), 16 B per line",
+                             "spread, 32 B per line (2 lanes)", "spread, 64 B per line (4 lanes)"};
+      printf("n=%zu wpg=%d %s: %d lines per env-step: %.3f us per step, %.0f G line-requests/s\n", n, wpg, what[sp], g,
+             best * 1e3 / steps, (double)n * g * steps / (best * 1e-3) / 1e9);
     }
     return 0;
   }
