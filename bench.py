@@ -18,13 +18,10 @@ the bytes a one-launch-per-step run leaves (tests/test_gpu_rollout.py).  No host
 max/sum of scalars (gloo).
 
 Also reported (rank 0; the extra lines only at N=1, so a scaling run stays short):
-  roofline       the dominant kernel k_env_rollout.  It is instruction-issue bound, not HBM
-                 bound: bound "valu-issue"; achieved = VALU wave-instructions per second (the
-                 per-wave-step VALU count of a rocprofv3 --pmc pass of this exact engine source,
-                 profiles/pmc_profile.json, x waves x steps / the launch time measured here with
-                 HIP events); peak = 1,024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU
-                 (MI355X_MICROARCH.md).  `hbm` holds the counter-measured HBM traffic (FETCH x 2
-                 + WRITE, gfx950 corrections) and SURVEY 8d's 800 B/env-step figure beside it.
+  roofline       the dominant kernel k_env_rollout against its store bound (bound "l2-store":
+                 the per-step output stores through L2, roofline() below); `hbm` holds the
+                 counter-measured HBM traffic (FETCH x 2 + WRITE, gfx950 corrections) and SURVEY
+                 8d's 800 B/env-step figure, `valu_issue` the VALU rate against the SIMDs' peak.
   shard_sizes    rollout us/step at the N=1 batch (65,536 on one GPU) and the N=8 shard (8,192)
   per_launch     one kernel launch per step (k_env_step<selected>)
   host_loop      the reference's numpy loop through the host API at C2 (256, EASY) and the C4
@@ -338,40 +335,59 @@ def cpu_baseline(seconds):
 
 
 def roofline(prof, n, k_chunk, launch_s):
+    """The dominant kernel k_env_rollout against what bounds it: its per-step output stores through
+    L2 (profiles/r03_store_bound.txt).  Every step stores the ~6.2 changed 16-B granules of each
+    env's records (ObsData tail, selected mask, Info byte, action); at 65,536 envs an XCD's share of
+    those lines exceeds its 4 MiB L2, so about half the stores miss and each costs a fabric
+    write-back.  Store bound of one launch: T_store = hits x c_hit + misses x c_miss, with the
+    launch's L2 write hits / misses from a rocprofv3 --pmc pass of this exact engine source and
+    c_hit / c_miss the measured cost of a scattered 16-B store that hits / misses L2 on this chip
+    (tools/storeprobe.hip, both in profiles/pmc_profile.json).  achieved = env-steps/s of the
+    launch timed here (HIP events); peak = env-steps/s if the launch took T_store; frac = T_store
+    / launch time.  Beside it: counter HBM traffic and the VALU issue rate (secondary bounds)."""
     waves = (n + 63) // 64
-    peak = N_SIMD * CLOCK_HZ / VALU_CYC                   # wave64 VALU instructions per second
-    out = {"bound": "valu-issue", "kernel": "k_env_rollout<selected>", "unit": "VALU wave-instr/s",
-           "peak": peak, "achieved": None, "frac": None, "traffic": None, "kernel_ms": launch_s * 1e3,
-           "steps_per_launch": k_chunk, "envs_per_launch": n}
+    valu_peak = N_SIMD * CLOCK_HZ / VALU_CYC                # wave64 VALU instructions per second
+    out = {"bound": "l2-store", "kernel": "k_env_rollout<selected>", "unit": "env-steps/s",
+           "achieved": n * k_chunk / launch_s, "peak": None, "frac": None, "traffic": None,
+           "kernel_ms": launch_s * 1e3, "steps_per_launch": k_chunk, "envs_per_launch": n}
     alg = STEP_BYTES * n * k_chunk
     out["hbm"] = {"survey_8d_bytes_per_launch": alg, "survey_8d_GBs": alg / launch_s / 1e9,
                   "note": "800 B/env-step (SURVEY 8d) assumes every step reads its state from HBM; "
                           "the rollout keeps it on-chip, so this rate can exceed the HBM peak"}
     r = (prof or {}).get("k_env_rollout")
+    key = str(k_chunk)
+    l2 = ((r or {}).get("l2_per_launch") or {}).get(key)
+    sc = (prof or {}).get("store_costs")
+    if l2 and sc and r.get("envs_per_launch") == n:
+        t_store = l2["hits"] * sc["c_hit_s"] + l2["misses"] * sc["c_miss_s"]
+        out.update(peak=n * k_chunk / t_store, frac=t_store / launch_s,
+                   store_model={"l2_write_requests_per_env_step": l2["writes"] / n / k_chunk,
+                                "l2_hits_per_launch": l2["hits"], "l2_misses_per_launch": l2["misses"],
+                                "fabric_write_requests_per_launch": l2.get("fabric_write_requests"),
+                                "c_hit_s": sc["c_hit_s"], "c_miss_s": sc["c_miss_s"],
+                                "t_store_s": t_store, "t_kernel_s": launch_s})
+    else:
+        out["note"] = "no PMC profile of this engine source at %d envs x %d steps (tools/pmc_profile.py): " \
+                      "store bound unknown" % (n, k_chunk)
     if r and r.get("valu_per_wave_step"):
         per_ws = r["valu_per_wave_step"]
         achieved = per_ws * waves * k_chunk / launch_s
-        out.update(achieved=achieved, frac=achieved / peak, valu_per_wave_step=per_ws,
-                   salu_per_wave_step=r.get("salu_per_wave_step"),
-                   issue_quads_per_wave_step=r.get("active_inst_any_per_wave_step"),
-                   wait_quads_per_wave_step=r.get("wait_any_per_wave_step"),
-                   wave_quads_per_wave_step=r.get("wave_cycles_per_wave_step"),
-                   lone_wave_frac=achieved / (peak / 2),
-                   issue_frac=(r.get("active_inst_any_per_wave_step") or 0) / max(r.get("wave_cycles_per_wave_step") or 1, 1),
-                   note="one 64-env wave per SIMD: a lone wave issues at most one instruction per 4 cycles "
-                        "(lone_wave_frac: VALU against that cap; issue_frac: quad-cycles issuing any "
-                        "instruction / wave lifetime, PMC); profiled at %d envs x %d steps per launch"
-                        % (r.get("envs_per_launch", 0), r.get("steps_per_launch", 0)))
+        out["valu_issue"] = {
+            "achieved": achieved, "peak": valu_peak, "frac": achieved / valu_peak, "unit": "VALU wave-instr/s",
+            "valu_per_wave_step": per_ws, "salu_per_wave_step": r.get("salu_per_wave_step"),
+            "issue_quads_per_wave_step": r.get("active_inst_any_per_wave_step"),
+            "wait_quads_per_wave_step": r.get("wait_any_per_wave_step"),
+            "wave_quads_per_wave_step": r.get("wave_cycles_per_wave_step"),
+            "note": "peak = 1,024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU; not the bound: a lone wave "
+                    "of this kernel uses about a quarter of its SIMD's VALU rate (profiled at %d envs x %d "
+                    "steps per launch)" % (r.get("envs_per_launch", 0), r.get("steps_per_launch", 0))}
         tr = r.get("bytes_per_step_launch", {})
-        key = str(k_chunk)
         if key in tr:
             out["traffic"] = tr[key]
             out["hbm"]["counter_GBs"] = tr[key] / launch_s / 1e9
             out["hbm"]["counter_frac"] = tr[key] / launch_s / 1e9 / HBM_PEAK_GBS
         elif "per_env_step" in r:
             out["hbm"]["counter_bytes_per_env_step"] = r["per_env_step"]
-    else:
-        out["note"] = "no PMC profile of this engine source (tools/pmc_profile.py): achieved unknown"
     return out
 
 

@@ -18,6 +18,7 @@ run sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_AC
 run fetch FETCH_SIZE && \
 run write WRITE_SIZE && \
 run l2 TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE && \
+run l2w TCC_WRITE_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum && \
 run inst SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM
 rc=$?
 python3 tools/pmc_summary.py "$OUT" > "$OUT/summary.txt" 2>&1

@@ -7,9 +7,13 @@ stamped with the hash of the engine source so that bench.py uses it only for the
 it measures.
 
     python tools/pmc_profile.py <dir of the K-step capture>:<K> [<dir>:<K> ...]  [--envs 65536]
+                                [--coeff <tools/store_coeff.sh output dir>]
 
 The first capture gives the per-wave-step instruction and cycle counts (use a long K); every
-capture gives the rollout's HBM bytes per launch at its K.
+capture gives the rollout's HBM bytes and L2 write hits / misses per launch at its K.  --coeff adds
+the store costs of bench.py's store roofline: seconds per L2-hitting and per L2-missing scattered
+16-B store, solved from tools/storeprobe's packed and spread patterns (their times and their
+counter-measured hits / misses).
 """
 import hashlib
 import json
@@ -46,7 +50,29 @@ def traffic(k):
     return 2.0 * k["FETCH_SIZE"] * 1024 + k["WRITE_SIZE"] * 1024
 
 
-def main(specs, envs=65536):
+def store_costs(d):
+    """Seconds per scattered 16-B store that hits / misses L2, from the packed and spread launches
+    of tools/storeprobe (coeff mode): t = hits x c_hit + misses x c_miss for each pattern."""
+    with open(os.path.join(d, "coeff.json")) as f:
+        c = json.loads(f.read().strip().splitlines()[-1])
+    res = summary(os.path.join(d, "pmc"))
+    pk = {k: v for k, v in res.items() if k.startswith("void k_store<1, 0, false>")}
+    sp = {k: v for k, v in res.items() if k.startswith("void k_store<1, 0, true>")}
+    (p,), (q,) = pk.values(), sp.values()
+    tp, ts = c["packed_us"] * 1e-6, c["spread_us"] * 1e-6
+    a11, a12, a21, a22 = p["TCC_HIT_sum"], p["TCC_MISS_sum"], q["TCC_HIT_sum"], q["TCC_MISS_sum"]
+    det = a11 * a22 - a12 * a21
+    c_hit = (tp * a22 - a12 * ts) / det
+    c_miss = (a11 * ts - a21 * tp) / det
+    return {"c_hit_s": c_hit, "c_miss_s": c_miss, "probe": c,
+            "packed": {"hits": a11, "misses": a12}, "spread": {"hits": a21, "misses": a22},
+            "note": "tools/storeprobe.hip coeff mode on MI355X: 65,536 envs of 17,216-B records, 6 scattered "
+                    "16-B stores per env-step into the record tails, 200 steps; packed = lines within L2, "
+                    "spread = lines beyond an XCD's 4 MiB L2; t = hits x c_hit + misses x c_miss solved "
+                    "from both"}
+
+
+def main(specs, envs=65536, coeff=None):
     waves = (envs + 63) // 64
     out = {"engine_sha": engine_hash(), "sources": specs,
            "method": "bytes = 2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024 (gfx950 corrections), mean per "
@@ -61,6 +87,10 @@ def main(specs, envs=65536):
             b = traffic(r)
             if b is not None:
                 ro["bytes_per_step_launch"][str(k)] = b
+            if "TCC_WRITE_sum" in r and "TCC_HIT_sum" in r:
+                ro.setdefault("l2_per_launch", {})[str(k)] = {
+                    "writes": r["TCC_WRITE_sum"], "hits": r["TCC_HIT_sum"], "misses": r["TCC_MISS_sum"],
+                    "fabric_write_requests": r.get("TCC_EA0_WRREQ_sum")}
             if j == 0:
                 per = lambda c: r[c] / waves / k if c in r else None   # noqa: E731
                 ro.update(steps_per_launch=k, valu_per_wave_step=per("SQ_INSTS_VALU"),
@@ -80,6 +110,8 @@ def main(specs, envs=65536):
                                   "valu_per_wave": kk.get("SQ_INSTS_VALU", 0) / max(1, kk.get("SQ_WAVES", 1)),
                                   "dispatches": kk["dispatches"]}
     out["k_env_rollout"] = ro
+    if coeff:
+        out["store_costs"] = store_costs(coeff)
     with open(os.path.join(ROOT, "profiles", "pmc_profile.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
@@ -94,4 +126,9 @@ if __name__ == "__main__":
         i = a.index("--envs")
         envs = int(a[i + 1])
         del a[i:i + 2]
-    main(a, envs)
+    coeff = None
+    if "--coeff" in a:
+        i = a.index("--coeff")
+        coeff = a[i + 1]
+        del a[i:i + 2]
+    main(a, envs, coeff)

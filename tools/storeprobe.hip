@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 constexpr size_t kObs = 17216, kTail = 16128;
 
@@ -50,6 +51,30 @@ __global__ void __launch_bounds__(256) k_store(uint8_t *obs, size_t n, int steps
   }
 }
 
+// The rollout's per-step output stores without the step (one env per work-item): per env-step
+// the phase granule, two granules of the acting player's deck, every other step a granule of its
+// stored mask or of the selected mask, the acting agent's Info steps byte and the 8-B action; the
+// acting player changes every 8 steps.  6 requests per env-step over ~4.7 lines, like the rollout.
+__global__ void __launch_bounds__(256) k_mimic(uint8_t *obs, uint8_t *sel, uint8_t *info, uint8_t *act, size_t n,
+                                               int steps) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  uint8_t *ob = obs + e * kObs;
+  uint4 v = make_uint4((uint32_t)e, 1u, 2u, 3u);
+  for (int t = 0; t < steps; t++) {
+    const int p = (t >> 3) & 3;
+    uint8_t *pr = ob + 16192 + 256 * p;
+    *reinterpret_cast<uint4 *>(ob + 16128) = v;
+    *reinterpret_cast<uint4 *>(pr + 16 * (t % 7)) = v;
+    *reinterpret_cast<uint4 *>(pr + 16 * ((t + 3) % 7)) = v;
+    if (t & 1) *reinterpret_cast<uint4 *>(pr + 128 + 16 * (t % 6)) = v;
+    else *reinterpret_cast<uint4 *>(sel + e * 128 + 16 * ((t >> 1) % 6)) = v;
+    info[e * 192 + 4 + 32 * p] = (uint8_t)t;
+    *reinterpret_cast<uint2 *>(act + e * 64) = make_uint2(v.x, (uint32_t)t);
+    v.y += 1u;
+  }
+}
+
 int main(int argc, char **argv) {
   const size_t n = argc > 1 ? strtoul(argv[1], nullptr, 10) : 65536;
   const int wpg = argc > 2 ? atoi(argv[2]) : 4;              // waves per workgroup
@@ -60,6 +85,46 @@ int main(int argc, char **argv) {
   hipEvent_t a, b;
   if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return 1;
   const dim3 grid((unsigned)((n / 64 + wpg - 1) / wpg)), blk(64 * wpg);
+  if (argc > 3 && !strcmp(argv[3], "coeff")) {             // the two store costs of bench.py's roofline
+    const int g = 6;
+    double us[2];
+    for (int sp = 0; sp < 2; sp++) {
+      float best = 1e30f;
+      for (int r = 0; r < 3; r++) {
+        if (hipEventRecord(a, 0) != hipSuccess) return 1;
+        if (sp) hipLaunchKernelGGL((k_store<1, 0, true>), grid, blk, 0, 0, obs, n, steps, g);
+        else hipLaunchKernelGGL((k_store<1, 0, false>), grid, blk, 0, 0, obs, n, steps, g);
+        if (hipEventRecord(b, 0) != hipSuccess || hipEventSynchronize(b) != hipSuccess) return 1;
+        float ms;
+        if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 1;
+        best = ms < best ? ms : best;
+      }
+      us[sp] = best * 1e3;
+    }
+    printf("{\"envs\": %zu, \"steps\": %d, \"stores_per_env_step\": %d, \"packed_us\": %.3f, \"spread_us\": %.3f}\n",
+           n, steps, g, us[0], us[1]);
+    return 0;
+  }
+  if (argc > 3 && !strcmp(argv[3], "mimic")) {
+    uint8_t *sel, *info, *act;
+    if (hipMalloc(&sel, n * 128) != hipSuccess || hipMalloc(&info, n * 192) != hipSuccess ||
+        hipMalloc(&act, n * 64) != hipSuccess)
+      return 1;
+    for (int ksteps : {20, 200, 1000}) {
+      float best = 1e30f;
+      for (int r = 0; r < 3; r++) {
+        if (hipEventRecord(a, 0) != hipSuccess) return 1;
+        hipLaunchKernelGGL(k_mimic, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, obs, sel, info, act, n, ksteps);
+        if (hipEventRecord(b, 0) != hipSuccess || hipEventSynchronize(b) != hipSuccess) return 1;
+        float ms;
+        if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 1;
+        best = ms < best ? ms : best;
+      }
+      printf("n=%zu mimic (the rollout's output stores, no step): %d steps per launch: %.3f us per step\n", n, ksteps,
+             best * 1e3 / ksteps);
+    }
+    return 0;
+  }
   if (argc > 3) {                                            // G granules per env-step, spread vs packed
     const int g = atoi(argv[3]);
     for (int sp = 0; sp < 4; sp++) {                       // packed, spread, spread 2 and 4 lanes per env
