@@ -463,13 +463,20 @@ def main():
         d.barrier_sync(runner)
         pl_wall = time.perf_counter() - t1
         pl_kern = kernel_time(runner, 1, pl_steps)
-        tr = ((prof or {}).get("k_env_step") or {}).get("bytes_per_launch")
+        ks = (prof or {}).get("k_env_step") or {}
+        tr = ks.get("bytes_per_launch")
         extras["per_launch"] = {"kernel": "k_env_step<selected>", "value": n * pl_steps / pl_wall,
                                 "ms_per_step": pl_wall / pl_steps * 1e3, "kernel_us": pl_kern * 1e6,
                                 "hbm": {"survey_8d_GBs": STEP_BYTES * n / pl_kern / 1e9,
                                         "survey_8d_frac": STEP_BYTES * n / pl_kern / 1e9 / HBM_PEAK_GBS,
                                         "traffic": tr,
                                         "counter_frac": (tr / pl_kern / 1e9 / HBM_PEAK_GBS) if tr else None}}
+        l2, sc = ks.get("l2_per_launch"), (prof or {}).get("store_costs")
+        if l2 and sc and ks.get("envs_per_launch") == n:       # the store bound (roofline() above)
+            t_store = l2["hits"] * sc["c_hit_s"] + l2["misses"] * sc["c_miss_s"]
+            extras["per_launch"]["l2_store"] = {"t_store_us": t_store * 1e6, "frac": t_store / pl_kern,
+                                                "l2_write_requests_per_env": (l2.get("writes") or 0) / n,
+                                                "l2_hits": l2["hits"], "l2_misses": l2["misses"]}
         runner.set_chunk(chunk)
         enc_ms = env.time_encode(20)
         enc_gbs = ENCODE_BYTES * n / (enc_ms / 1e3) / 1e9

@@ -109,6 +109,10 @@ def main(specs, envs=65536, coeff=None):
                     out[short] = {"envs_per_launch": envs, "bytes_per_launch": traffic(kk),
                                   "valu_per_wave": kk.get("SQ_INSTS_VALU", 0) / max(1, kk.get("SQ_WAVES", 1)),
                                   "dispatches": kk["dispatches"]}
+                    if "TCC_HIT_sum" in kk:
+                        out[short]["l2_per_launch"] = {"writes": kk.get("TCC_WRITE_sum"), "hits": kk["TCC_HIT_sum"],
+                                                       "misses": kk["TCC_MISS_sum"],
+                                                       "fabric_write_requests": kk.get("TCC_EA0_WRREQ_sum")}
     out["k_env_rollout"] = ro
     if coeff:
         out["store_costs"] = store_costs(coeff)
