@@ -44,13 +44,27 @@ def _run(cmd, cwd=None):
     subprocess.run(cmd, check=True, cwd=cwd)
 
 
+OBJ = os.path.join(PKG, "build")
+HEADERS = [os.path.join(CSRC, f) for f in ("cog_engine.h", "cog_tables.h", "cog_rng.h")] + [
+    os.path.join(INCLUDE, f) for f in ("cog.h", "cog_types.h")]
+
+
 def build_engine(force=False):
-    if force or _stale(LIB, ENGINE_DEPS):
-        # max-ilp scheduling: the rollout runs one wave per SIMD, so only instruction-level
-        # parallelism hides latency (1 % faster than the default, tools/flags_exp.sh)
-        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-ffp-contract=off", "-mllvm", "-amdgpu-sched-strategy=max-ilp", "-Wall",
-              f"-I{INCLUDE}", f"-I{CSRC}", *ENGINE_SRCS, "-o", LIB])
+    """One object per source (the kernels' TU takes about two minutes, the ABI's seconds), then
+    the shared library."""
+    os.makedirs(OBJ, exist_ok=True)
+    objs = []
+    for src in ENGINE_SRCS:
+        obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [src] + HEADERS):
+            # max-ilp scheduling: the rollout runs one wave per SIMD, so only instruction-level
+            # parallelism hides latency (1 % faster than the default, tools/flags_exp.sh)
+            _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c",
+                  "-ffp-contract=off", "-mllvm", "-amdgpu-sched-strategy=max-ilp", "-Wall",
+                  f"-I{INCLUDE}", f"-I{CSRC}", src, "-o", obj])
+    if force or _stale(LIB, objs):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB])
     return LIB
 
 

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -159,6 +160,68 @@ bool zc_same_on(int device, const void *p) {
   return ok;
 }
 
+// Completion of a host call.  A synchronous call queues k_signal(seq) behind its work and spins
+// on the pinned word it stores, instead of hipStreamSynchronize: the word lands about 2.5 us
+// before the runtime's own completion signal would wake a stream sync, and a stream sync after
+// the spin would wait for that signal again (+8 us measured: profiles/r03_latprobe.txt).  Only
+// calls whose results are in device memory or in the engine's pinned views use it (no pageable
+// copy is pending).  After spin_us without the word (a long call, or a fault that keeps the
+// signal from running), the call falls back to hipStreamSynchronize, which reports errors.
+// $COG_SPIN_US sets the spin budget (default 2,000 us; 0: always hipStreamSynchronize).
+// A call whose last kernel can store the word itself (k_sample, k_publish: GridSignal, the last
+// workgroup through a device counter) arms it instead (signal_arm / signal_armed): one dependent
+// dispatch less, about 3 us.
+struct Signal {
+  volatile uint32_t *h = nullptr;     // host address of the word
+  uint32_t *d = nullptr;              // its device address
+  uint32_t *ctr = nullptr;            // device counter of the in-kernel form (zero between calls)
+  uint32_t seq = 0;
+  bool queued = false;                // a store of seq is queued on the stream
+};
+long spin_budget_us() {
+  static const long v = [] {
+    const char *e = std::getenv("COG_SPIN_US");
+    return e ? std::max(0L, std::atol(e)) : 2000L;
+  }();
+  return v;
+}
+// the counter and seq for a kernel that stores the word itself (null: no spinning)
+uint32_t *signal_arm(const Signal &g, uint32_t &seq) {
+  if (!g.d || !g.ctr || spin_budget_us() <= 0) return nullptr;
+  seq = g.seq + 1;
+  return g.ctr;
+}
+void signal_armed(Signal &g) {        // (after the kernel that stores it was launched)
+  g.seq++;
+  g.queued = true;
+}
+int signal_enqueue(Signal &g, hipStream_t st) {
+  if (g.queued) return COG_OK;                             // (armed in the call's last kernel)
+  if (!g.d || spin_budget_us() <= 0) return COG_OK;
+  if (cog::launch_signal(g.d, g.seq + 1, st)) {            // (not queued: the wait syncs the stream)
+    (void)hipGetLastError();
+    return COG_OK;
+  }
+  g.seq++;
+  g.queued = true;
+  return COG_OK;
+}
+int signal_wait(Signal &g, hipStream_t st) {
+  if (g.queued) {
+    g.queued = false;
+    if (*g.h == g.seq) return COG_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    const auto budget = std::chrono::microseconds(spin_budget_us());
+    for (unsigned it = 1;; it++) {
+      if (*g.h == g.seq) return COG_OK;
+      __builtin_ia32_pause();
+      if (!(it & 255u) && std::chrono::steady_clock::now() - t0 > budget) break;
+    }
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  return COG_OK;
+}
+
 // the reference runner's block split (runner.h:33-38): n / k per block, the last takes the rest
 std::vector<size_t> block_split(size_t n, int k) {
   std::vector<size_t> first(k + 1);
@@ -199,6 +262,7 @@ struct EnvShard {
   bool zc = false;
   uint8_t *h_obs_d = nullptr, *h_outs_d = nullptr, *mir = nullptr;
   bool mir_valid = false;
+  Signal done;                        // completion word: word 32 of the shard's error line
 };
 
 struct cog_env {
@@ -224,12 +288,14 @@ struct SamplerShard {
   uint32_t *d_rng = nullptr;
   uint8_t *d_actions = nullptr;
   uint8_t *d_masks = nullptr;         // staging for host-provided masks
+  Signal done;                        // completion word (cog_sampler::h_sig)
 };
 
 struct cog_sampler {
   size_t n = 0;
   std::vector<SamplerShard> sh;
   cog_action_t *h_actions = nullptr;  // persistent pinned view, all shards
+  uint32_t *h_sig = nullptr;          // pinned, device-mapped: one completion word per shard (256 B apart)
 };
 
 struct cog_runner {
@@ -255,7 +321,7 @@ void env_free(cog_env *e) {
     DeviceGuard g(k.device);
     if (k.stream) (void)hipStreamSynchronize(k.stream);
     void *dev[] = {k.s.obs, k.outs, k.s.priv, k.s.grid, k.s.cgrid, k.s.heads, k.s.gen, k.s.dirty, k.d_actions, k.mir,
-                   k.s.park};
+                   k.s.park, k.done.ctr};
     for (void *p : dev)
       if (p) (void)hipFree(p);
     zc_free(k.h_outs);
@@ -275,6 +341,22 @@ int sync_all(cog_env *e) {
   for (EnvShard &k : e->sh) {
     DeviceGuard g(k.device);
     HIPCHK(hipStreamSynchronize(k.stream));
+  }
+  return COG_OK;
+}
+
+// sync_all through the completion words: for calls whose results are in device memory or in
+// pinned views (no pageable copy pending)
+int sync_fast(cog_env *e) {
+  for (EnvShard &k : e->sh) {
+    DeviceGuard g(k.device);
+    int rc = signal_enqueue(k.done, k.stream);
+    if (rc) return rc;
+  }
+  for (EnvShard &k : e->sh) {
+    DeviceGuard g(k.device);
+    int rc = signal_wait(k.done, k.stream);
+    if (rc) return rc;
   }
   return COG_OK;
 }
@@ -324,9 +406,12 @@ void gather_small(cog_env *e) {
 int enqueue_publish(EnvShard &k, const SamplerShard *q, uint8_t *h_act_d) {
   if (!k.n) return COG_OK;
   const OutLayout L(k.n);
+  uint32_t seq = 0;
+  uint32_t *ctr = cog::publish_can_signal(k.n, L.alloc, q && h_act_d) ? signal_arm(k.done, seq) : nullptr;
   if (cog::launch_publish(k.s, k.outs, k.mir, k.h_obs_d, k.h_outs_d, L.alloc, k.mir_valid ? 0 : 1,
-                          q ? q->d_actions : nullptr, q ? h_act_d : nullptr, k.stream))
+                          q ? q->d_actions : nullptr, q ? h_act_d : nullptr, k.stream, ctr, k.done.d, seq))
     return fail(COG_ERR_HIP, std::string("publish launch failed: ") + hipGetErrorString(hipGetLastError()));
+  if (ctr) signal_armed(k.done);
   k.mir_valid = true;
   return COG_OK;
 }
@@ -334,6 +419,7 @@ int enqueue_publish(EnvShard &k, const SamplerShard *q, uint8_t *h_act_d) {
 // smp (optional): a runner's sampler whose actions' host view is refreshed with the env's
 int finish(cog_env *e, bool refresh_host, cog_sampler *smp = nullptr) {
   const bool host = refresh_host && e->host;
+  for (EnvShard &k : e->sh) k.done.queued = false;        // (a failed call may have left one armed)
   for (size_t j = 0; j < e->sh.size(); j++) {
     EnvShard &k = e->sh[j];
     DeviceGuard g(k.device);
@@ -354,7 +440,7 @@ int finish(cog_env *e, bool refresh_host, cog_sampler *smp = nullptr) {
     }
     if (rc) return rc;
   }
-  int rc = sync_all(e);
+  int rc = sync_fast(e);
   if (rc) return rc;
   uint32_t flags = 0, errors = 0;
   bool any_dirty = false;
@@ -440,12 +526,13 @@ void sampler_free(cog_sampler *s) {
   for (SamplerShard &k : s->sh) {
     DeviceGuard g(k.device);
     if (k.stream) (void)hipStreamSynchronize(k.stream);
-    void *dev[] = {k.d_rng, k.d_actions, k.d_masks};
+    void *dev[] = {k.d_rng, k.d_actions, k.d_masks, k.done.ctr};
     for (void *p : dev)
       if (p) (void)hipFree(p);
     if (k.stream) (void)hipStreamDestroy(k.stream);
   }
   zc_free(s->h_actions);
+  if (s->h_sig) (void)hipHostFree(s->h_sig);
   delete s;
 }
 
@@ -471,7 +558,7 @@ int env_shard_init(EnvShard &k, uint32_t default_seed, uint32_t *err_word) {
       (rc = dmalloc(&s.cgrid, n * (size_t)COG_CELLS)) || (rc = dmalloc(&s.heads, n * 5 * sizeof(uint4))) ||
       (rc = dmalloc(&s.gen, n * sizeof(cog::GenScratch))) || (rc = dmalloc(&s.dirty, n * sizeof(uint32_t))) ||
       (rc = dmalloc(&k.d_actions, n * COG_ACTION_BYTES)) || (rc = dmalloc(&s.park, n * sizeof(uint32_t))) ||
-      (rc = zc_alloc(&k.h_outs, L.alloc)))
+      (rc = dmalloc(&k.done.ctr, 256)) || (rc = zc_alloc(&k.h_outs, L.alloc)))
     return rc;
   std::memset(k.h_outs, 0, L.alloc);
   s.n = n;
@@ -487,9 +574,11 @@ int env_shard_init(EnvShard &k, uint32_t default_seed, uint32_t *err_word) {
   void *d_err = nullptr;
   HIPCHK(hipHostGetDevicePointer(&d_err, err_word, 0));
   s.err = static_cast<uint32_t *>(d_err);
+  k.done.h = err_word + 32;
+  k.done.d = s.err + 32;
   struct { void *p; size_t b; } z[] = {{s.obs, n * COG_OBS_BYTES}, {k.outs, L.alloc}, {s.grid, n * (size_t)cog::kGridBytes},
                                        {s.cgrid, n * (size_t)COG_CELLS}, {s.gen, n * sizeof(cog::GenScratch)},
-                                       {k.d_actions, n * COG_ACTION_BYTES}};
+                                       {k.d_actions, n * COG_ACTION_BYTES}, {k.done.ctr, 256}};
   for (auto &zz : z)
     if (zz.b) HIPCHK(hipMemsetAsync(zz.p, 0, zz.b, k.stream));
   if (n) HIPCHK(hipMemsetAsync(s.park, 0xff, n * sizeof(uint32_t), k.stream));   // no env parked
@@ -581,13 +670,14 @@ int cog_env_shard_info(const cog_env *env, int k, size_t *first, size_t *count, 
 static int env_reset_impl(cog_env *e, const cog::ResetParams &p) {
   int rc = prepare_host(e);
   if (rc) return rc;
+  for (EnvShard &k : e->sh) k.done.queued = false;
   for (EnvShard &k : e->sh) {
     DeviceGuard g(k.device);
     if (cog::launch_reset(k.s, p, k.stream) || cog::launch_encode_all(k.s, k.stream))
       return fail(COG_ERR_HIP, std::string("reset launch failed: ") + hipGetErrorString(hipGetLastError()));
     if ((rc = enqueue_status_only(k))) return rc;
   }
-  if ((rc = sync_all(e))) return rc;
+  if ((rc = sync_fast(e))) return rc;
   uint32_t flags = 0, errors = 0;
   for (size_t j = 0; j < e->sh.size(); j++) {
     EnvShard &k = e->sh[j];
@@ -887,6 +977,11 @@ int cog_sampler_create_multi(size_t n_envs, uint64_t seed, const int *devices, i
     return rc;
   }
   std::memset(s->h_actions, 0, n_envs * COG_ACTION_BYTES);
+  if ((rc = hmalloc(&s->h_sig, 256 * (size_t)n_devices, hipHostMallocMapped | hipHostMallocCoherent))) {
+    sampler_free(s);
+    return rc;
+  }
+  std::memset(s->h_sig, 0, 256 * (size_t)n_devices);
   const std::vector<size_t> first = block_split(n_envs, n_devices);
   s->sh.resize(n_devices);
   for (int j = 0; j < n_devices; j++) {
@@ -900,12 +995,18 @@ int cog_sampler_create_multi(size_t n_envs, uint64_t seed, const int *devices, i
       return fail(COG_ERR_HIP, "hipStreamCreate failed");
     }
     if ((rc = dmalloc(&k.d_rng, k.n * sizeof(uint32_t))) || (rc = dmalloc(&k.d_actions, k.n * COG_ACTION_BYTES)) ||
-        (rc = dmalloc(&k.d_masks, k.n * COG_MASK_BYTES))) {
+        (rc = dmalloc(&k.d_masks, k.n * COG_MASK_BYTES)) || (rc = dmalloc(&k.done.ctr, 256))) {
       sampler_free(s);
       return rc;
     }
+    void *d_sig = nullptr;
+    if (hipHostGetDevicePointer(&d_sig, s->h_sig + 64 * j, 0) == hipSuccess) {
+      k.done.h = s->h_sig + 64 * j;
+      k.done.d = static_cast<uint32_t *>(d_sig);
+    }
     // vec_action_sampler(seed) (vec_sampler.h:9-13): sampler i seeded seed + i, seed a u32
     if (hipMemsetAsync(k.d_actions, 0, k.n * COG_ACTION_BYTES, k.stream) != hipSuccess ||
+        hipMemsetAsync(k.done.ctr, 0, 256, k.stream) != hipSuccess ||
         cog::launch_seed_sampler(k.n, (uint64_t)(uint32_t)seed, k.first, k.d_rng, k.stream)) {
       sampler_free(s);
       return fail(COG_ERR_HIP, "sampler init failed");
@@ -934,12 +1035,17 @@ int cog_sampler_num_shards(const cog_sampler *s, int *out) {
   return COG_OK;
 }
 
+// signal: the sampler kernel stores the shard's completion word (host calls on the sampler's
+// own stream)
 static int sampler_run(SamplerShard &k, cog_action_t *h_actions, const uint8_t *d_masks, hipStream_t stream,
-                       bool host_refresh) {
+                       bool host_refresh, bool signal = false) {
   uint8_t *h_act = host_refresh && k.n ? const_cast<uint8_t *>(zc_device(h_actions + k.first, k.n * COG_ACTION_BYTES)) : nullptr;
   if (h_act && !zc_same_on(k.device, h_actions)) h_act = nullptr;
-  if (cog::launch_sample(k.n, d_masks, k.d_rng, k.d_actions, stream, h_act))   // actions to the host view in place
+  uint32_t seq = 0;
+  uint32_t *ctr = signal && h_act ? signal_arm(k.done, seq) : nullptr;
+  if (cog::launch_sample(k.n, d_masks, k.d_rng, k.d_actions, stream, h_act, ctr, k.done.d, seq))   // actions to the host view in place
     return fail(COG_ERR_HIP, std::string("sample launch failed: ") + hipGetErrorString(hipGetLastError()));
+  if (ctr) signal_armed(k.done);
   if (host_refresh && k.n && !h_act)
     HIPCHK(hipMemcpyAsync(h_actions + k.first, k.d_actions, k.n * COG_ACTION_BYTES, hipMemcpyDeviceToHost, stream));
   return COG_OK;
@@ -951,15 +1057,16 @@ int cog_sampler_sample_device(cog_sampler *s, const void *d_masks, size_t n) {
   if (s->sh.size() != 1) return fail(COG_ERR_INVALID, "device masks need a single-shard sampler (one device pointer)");
   SamplerShard &k = s->sh[0];
   DeviceGuard g(k.device);
-  int rc = sampler_run(k, s->h_actions, static_cast<const uint8_t *>(d_masks), k.stream, true);
-  if (rc) return rc;
-  HIPCHK(hipStreamSynchronize(k.stream));
-  return COG_OK;
+  k.done.queued = false;
+  int rc = sampler_run(k, s->h_actions, static_cast<const uint8_t *>(d_masks), k.stream, true, true);
+  if (rc || (rc = signal_enqueue(k.done, k.stream))) return rc;
+  return signal_wait(k.done, k.stream);
 }
 
 int cog_sampler_sample(cog_sampler *s, const cog_action_mask_t *masks, size_t n) {
   if (!s || (!masks && n)) return fail(COG_ERR_INVALID, "NULL argument");
   if (n != s->n) return fail(COG_ERR_INVALID, "action_mask length != num_envs");
+  for (SamplerShard &k : s->sh) k.done.queued = false;
   for (SamplerShard &k : s->sh) {
     if (!k.n) continue;
     DeviceGuard g(k.device);
@@ -968,12 +1075,13 @@ int cog_sampler_sample(cog_sampler *s, const cog_action_mask_t *masks, size_t n)
       HIPCHK(hipMemcpyAsync(k.d_masks, masks + k.first, k.n * COG_MASK_BYTES, hipMemcpyHostToDevice, k.stream));
       dm = k.d_masks;
     }
-    int rc = sampler_run(k, s->h_actions, dm, k.stream, true);
-    if (rc) return rc;
+    int rc = sampler_run(k, s->h_actions, dm, k.stream, true, true);
+    if (rc || (rc = signal_enqueue(k.done, k.stream))) return rc;
   }
   for (SamplerShard &k : s->sh) {
     DeviceGuard g(k.device);
-    HIPCHK(hipStreamSynchronize(k.stream));
+    int rc = signal_wait(k.done, k.stream);
+    if (rc) return rc;
   }
   return COG_OK;
 }

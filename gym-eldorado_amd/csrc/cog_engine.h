@@ -121,19 +121,28 @@ int launch_init(const DevState &s, const uint32_t *seeds_host_unused, uint32_t d
 int launch_reset(const DevState &s, const ResetParams &p, void *stream);
 int launch_encode_all(const DevState &s, void *stream, int variant = 0);
 int launch_step(const DevState &s, const uint8_t *d_actions, void *stream);
+// h_actions: device-mapped host view (or null); sig_ctr (or null), sig_word, seq: the in-kernel
+// completion word (the last workgroup stores seq into *sig_word; sig_ctr a zeroed device counter)
 int launch_sample(size_t n, const uint8_t *d_masks, uint32_t *d_rng, uint8_t *d_actions,
-                  void *stream, uint8_t *h_actions = nullptr);   // h_actions: device-mapped host view (or null)
+                  void *stream, uint8_t *h_actions = nullptr, uint32_t *sig_ctr = nullptr,
+                  uint32_t *sig_word = nullptr, uint32_t seq = 0);
 // the host views' dynamic records from HBM: granules that differ from `mir` (an HBM copy of the
 // host views) are stored into the device-mapped pinned views h_obs / h_outs (and into mir);
 // outs_bytes a multiple of 16; force = 1 stores every granule; d_actions / h_actions optional
 int launch_publish(const DevState &s, const uint8_t *outs, uint8_t *mir, uint8_t *h_obs, uint8_t *h_outs,
-                   size_t outs_bytes, int force, const uint8_t *d_actions, uint8_t *h_actions, void *stream);
+                   size_t outs_bytes, int force, const uint8_t *d_actions, uint8_t *h_actions, void *stream,
+                   uint32_t *sig_ctr = nullptr, uint32_t *sig_word = nullptr, uint32_t seq = 0);
 size_t publish_mirror_bytes(size_t n, size_t outs_bytes);
+// whether launch_publish may store a completion word itself (its grid is small enough)
+bool publish_can_signal(size_t n, size_t outs_bytes, bool actions);
 int launch_sample_step(const DevState &s, int mask_source, uint32_t *d_rng, uint8_t *d_actions,
                        void *stream);
 int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions,
                    void *stream);                    // persistent K-step runner loop
 int launch_seed_sampler(size_t n, uint64_t seed, size_t first, uint32_t *d_rng, void *stream);
+// completion word: stores seq into *d_word (device address of a pinned host word) once every
+// earlier packet of the stream has completed
+int launch_signal(uint32_t *d_word, uint32_t seq, void *stream);
 // variant bit 0: non-temporal loads/stores; bit 1: 32 waves per CU instead of 8 (grid stride);
 // bit 2: one pass, 32 KiB per workgroup (bit 1 ignored); bytes: a multiple of 16
 int launch_copy_peak(const void *src, void *dst, size_t bytes, void *stream, int variant);

@@ -3229,21 +3229,45 @@ __global__ void __launch_bounds__(64) k_env_fixup(DevState s, int steps, uint32_
   }
 }
 
+// In-kernel completion word of a host call (the host spins on it, cog_abi.cpp Signal): the last
+// workgroup to finish stores `seq` into the pinned word, after every workgroup's stores (device
+// records and the host views) have been acknowledged.  A counter in device memory finds the last
+// workgroup (about 14 ns per arriving workgroup on one address, tools/latprobe.hip), so kernels
+// that signal keep their grids small; the last workgroup re-arms the counter.
+struct GridSignal {
+  uint32_t *ctr;                      // device counter (0 between calls); null: no signal
+  uint32_t *word;                     // device address of the pinned host word
+  uint32_t seq;
+};
+DEV void grid_signal(const GridSignal &g) {
+  if (!g.ctr) return;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();                                       // this workgroup's stores performed
+    if (atomicAdd(g.ctr, 1u) == gridDim.x - 1) {
+      __hip_atomic_store(g.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(g.word, g.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 // masks may be device memory or pinned host memory (zero-copy); h_actions (may be null) is the
 // host view of the actions, written straight over PCIe beside the device copy
 __global__ void __launch_bounds__(256) k_sample(size_t n, const uint8_t *__restrict__ masks,
                                                 uint32_t *__restrict__ rngs, uint8_t *__restrict__ actions,
-                                                uint8_t *__restrict__ h_actions) {
+                                                uint8_t *__restrict__ h_actions, GridSignal sig) {
   __shared__ UidEntry tab[kUidTab];
   uid_tab_fill(tab);
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t rng = rngs[i];
-  uint8_t a[5];
-  sample_mask(masks + i * COG_MASK_BYTES, rng, a, tab);
-  rngs[i] = rng;
-  store_action(actions + i * COG_ACTION_BYTES, a);
-  if (h_actions) store_action(h_actions + i * COG_ACTION_BYTES, a);
+  if (i < n) {
+    uint32_t rng = rngs[i];
+    uint8_t a[5];
+    sample_mask(masks + i * COG_MASK_BYTES, rng, a, tab);
+    rngs[i] = rng;
+    store_action(actions + i * COG_ACTION_BYTES, a);
+    if (h_actions) store_action(h_actions + i * COG_ACTION_BYTES, a);
+  }
+  grid_signal(sig);
 }
 
 // Host views without copy commands: the dynamic part of every host-visible record -- the ObsData
@@ -3258,35 +3282,70 @@ __global__ void __launch_bounds__(256) k_sample(size_t n, const uint8_t *__restr
 // sampler's actions (the 8 bytes store_action writes at the head of each 64-B record) ride along
 // when act is given.
 constexpr size_t kRecG = COG_OBS_BYTES / 16, kTail0 = COG_OBS_MAP_BYTES / 16, kTailG = kRecG - kTail0;
+// Two granules per work-item, both loaded before either is compared (all loads in flight), so
+// that a small batch's grid is small enough for the in-kernel completion word (<= 128 workgroups:
+// 256 envs take 46); larger grids are signalled by k_signal after the kernel.
+constexpr unsigned kPublishPerItem = 2, kPublishSignalBlocks = 128;
 __global__ void __launch_bounds__(256) k_publish(const uint4 *__restrict__ obs, const uint4 *__restrict__ outs,
                                                  uint4 *__restrict__ mir, uint4 *__restrict__ h_obs,
                                                  uint4 *__restrict__ h_outs, size_t n, size_t outs_g, int force,
-                                                 const uint2 *__restrict__ act, uint2 *__restrict__ h_act) {
-  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t tail = n * kTailG;
-  if (t < tail) {
-    const size_t row = t / kTailG, a = row * kRecG + kTail0 + (t - kTailG * row);
-    const uint4 c = obs[a];
-    if (force || ne4(c, mir[t])) {
-      h_obs[a] = c;
-      mir[t] = c;
+                                                 const uint2 *__restrict__ act, uint2 *__restrict__ h_act,
+                                                 GridSignal sig) {
+  const size_t tail = n * kTailG, ng = tail + outs_g;
+  const size_t t0 = ((size_t)blockIdx.x * blockDim.x) * kPublishPerItem + threadIdx.x;
+  const uint4 *src[kPublishPerItem];
+  uint4 *dst[kPublishPerItem];
+  uint4 c[kPublishPerItem], m[kPublishPerItem];
+  bool cmp[kPublishPerItem];
+#pragma unroll
+  for (unsigned j = 0; j < kPublishPerItem; j++) {         // granule t of the views: a tail or outs granule
+    const size_t t = t0 + (size_t)j * blockDim.x;
+    src[j] = nullptr;
+    if (t < tail) {
+      const size_t row = t / kTailG, a = row * kRecG + kTail0 + (t - kTailG * row);
+      src[j] = obs + a;
+      dst[j] = h_obs + a;
+      cmp[j] = !force;
+    } else if (t < ng) {
+      const size_t u = t - tail;
+      src[j] = outs + u;
+      dst[j] = h_outs + u;
+      cmp[j] = !force && u >= 4;                           // (the status granules always go)
     }
-  } else if (t < tail + outs_g) {
-    const size_t u = t - tail;
-    const uint4 c = outs[u];
-    if (force || u < 4 || ne4(c, mir[t])) {
-      h_outs[u] = c;
-      mir[t] = c;
+    if (src[j]) {
+      c[j] = *src[j];
+      if (cmp[j]) m[j] = mir[t];
     }
-  } else if (act && t < tail + outs_g + n) {
-    const size_t i = t - tail - outs_g;
+  }
+#pragma unroll
+  for (unsigned j = 0; j < kPublishPerItem; j++) {
+    const size_t t = t0 + (size_t)j * blockDim.x;
+    if (src[j] && (!cmp[j] || ne4(c[j], m[j]))) {
+      *dst[j] = c[j];
+      mir[t] = c[j];
+    }
+  }
+  // the sampler's actions: one work-item per env after the granules
+  const size_t ia = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t g_items = (ng + kPublishPerItem - 1) / kPublishPerItem;
+  if (act && ia >= g_items && ia - g_items < n) {
+    const size_t i = ia - g_items;
     h_act[(COG_ACTION_BYTES / 8) * i] = act[(COG_ACTION_BYTES / 8) * i];
   }
+  grid_signal(sig);
 }
 
 __global__ void k_sync_heads(DevState s) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < s.n) sync_heads(s, i);
+}
+
+// Completion word of a host call: queued behind the call's work on its stream, it stores `seq`
+// into a pinned, device-mapped word that the host spins on (a system-scope release store, after
+// every earlier packet of the stream has completed).  The host learns completion about 2.5 us
+// sooner than through hipStreamSynchronize (tools/latprobe.hip, profiles/r03_latprobe.txt).
+__global__ void __launch_bounds__(64) k_signal(uint32_t *word, uint32_t seq) {
+  if (threadIdx.x == 0) __hip_atomic_store(word, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ void k_seed_sampler(size_t n, uint64_t seed, size_t first, uint32_t *rngs) {
@@ -3380,10 +3439,10 @@ int launch_step(const DevState &s, const uint8_t *d_actions, void *stream) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_sample(size_t n, const uint8_t *d_masks, uint32_t *d_rng, uint8_t *d_actions, void *stream,
-                  uint8_t *h_actions) {
+                  uint8_t *h_actions, uint32_t *sig_ctr, uint32_t *sig_word, uint32_t seq) {
   if (!n) return 0;
   hipLaunchKernelGGL(k_sample, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, n, d_masks, d_rng, d_actions,
-                     h_actions);
+                     h_actions, GridSignal{sig_ctr, sig_word, seq});
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_sample_step(const DevState &s, int mask_source, uint32_t *d_rng, uint8_t *d_actions, void *stream) {
@@ -3453,15 +3512,27 @@ int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rn
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+// work-items: granule pairs (a workgroup covers 512 consecutive granules), then one per action
+static unsigned publish_blocks(size_t n, size_t outs_bytes, bool actions) {
+  const size_t ng = n * kTailG + outs_bytes / 16;
+  return blocks_for((ng + kPublishPerItem - 1) / kPublishPerItem + (actions ? n : 0), 256);
+}
 int launch_publish(const DevState &s, const uint8_t *outs, uint8_t *mir, uint8_t *h_obs, uint8_t *h_outs, size_t outs_bytes,
-                   int force, const uint8_t *d_actions, uint8_t *h_actions, void *stream) {
+                   int force, const uint8_t *d_actions, uint8_t *h_actions, void *stream, uint32_t *sig_ctr,
+                   uint32_t *sig_word, uint32_t seq) {
   if (!s.n) return 0;
-  const size_t outs_g = outs_bytes / 16, threads = s.n * kTailG + outs_g + (d_actions ? s.n : 0);
-  hipLaunchKernelGGL(k_publish, dim3(blocks_for(threads, 256)), dim3(256), 0, (hipStream_t)stream,
+  const unsigned blocks = publish_blocks(s.n, outs_bytes, d_actions != nullptr);
+  if (sig_ctr && blocks > kPublishSignalBlocks) return -1; // (publish_can_signal says no)
+  const size_t outs_g = outs_bytes / 16;
+  hipLaunchKernelGGL(k_publish, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
                      reinterpret_cast<const uint4 *>(s.obs), reinterpret_cast<const uint4 *>(outs),
                      reinterpret_cast<uint4 *>(mir), reinterpret_cast<uint4 *>(h_obs), reinterpret_cast<uint4 *>(h_outs),
-                     s.n, outs_g, force, reinterpret_cast<const uint2 *>(d_actions), reinterpret_cast<uint2 *>(h_actions));
+                     s.n, outs_g, force, reinterpret_cast<const uint2 *>(d_actions), reinterpret_cast<uint2 *>(h_actions),
+                     GridSignal{sig_ctr, sig_word, seq});
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+bool publish_can_signal(size_t n, size_t outs_bytes, bool actions) {
+  return publish_blocks(n, outs_bytes, actions) <= kPublishSignalBlocks;
 }
 size_t publish_mirror_bytes(size_t n, size_t outs_bytes) { return n * kTailG * 16 + outs_bytes; }
 int launch_copy_peak(const void *src, void *dst, size_t bytes, void *stream, int variant) {
@@ -3477,6 +3548,10 @@ int launch_copy_peak(const void *src, void *dst, size_t bytes, void *stream, int
   const dim3 g(variant & 2 ? 8192 : 2048), t(256);   // grid stride: 8 or 32 waves per CU
   if (variant & 1) hipLaunchKernelGGL(k_copy_peak<true>, g, t, 0, (hipStream_t)stream, a, b, n16);
   else hipLaunchKernelGGL(k_copy_peak<false>, g, t, 0, (hipStream_t)stream, a, b, n16);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int launch_signal(uint32_t *d_word, uint32_t seq, void *stream) {
+  hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, (hipStream_t)stream, d_word, seq);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_seed_sampler(size_t n, uint64_t seed, size_t first, uint32_t *d_rng, void *stream) {
