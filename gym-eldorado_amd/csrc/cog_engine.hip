@@ -2338,16 +2338,16 @@ DEV void store_changes(const DevState &s, size_t i, int ag, int na, const Snap &
 
 // the action of this step: sampled (runner) or the host's (indices past a head are the
 // reference's out-of-range accesses: clamped and flagged)
+// (ext: MASK_EXTERNAL's ActionData bytes 0..7, loaded by the caller at the start of the step)
 template <int SRC>
-DEV void step_action(RegEnv &R, const uint8_t *act_in, size_t i, uint32_t &srng, uint8_t act[5]) {
+DEV void step_action(RegEnv &R, const uint2 &ext, uint32_t &srng, uint8_t act[5]) {
   if (SRC == MASK_SELECTED) sample_heads(R.sel, srng, act, R.tab);
   else if (SRC == MASK_STORED) sample_heads(R.sta, srng, act, R.tab);
   else {
-    const uint8_t *ai = act_in + i * COG_ACTION_BYTES;
     const uint8_t top[5] = {COG_N_CARDTYPES, COG_N_CARDTYPES, COG_N_CARDTYPES, 6, COG_N_SHOP};
 #pragma unroll
     for (int k = 0; k < 5; k++) {
-      act[k] = ai[k];
+      act[k] = (uint8_t)((k < 4 ? ext.x >> (8 * k) : ext.y) & 0xffu);
       if (act[k] > top[k]) {
         act[k] = top[k];
         R.flags |= F_BAD_ACTION;
@@ -2405,6 +2405,10 @@ DEV bool env_step_lane(const DevState &s, size_t i, const uint8_t *act_in, uint3
   PH_DECL;
   Snap S;
   RegEnv R;
+  // the host's action first: often pinned host memory read over PCIe, its latency then overlaps
+  // the state loads' instead of adding a round after them
+  uint2 ext = make_uint2(0u, 0u);
+  if (SRC == MASK_EXTERNAL) ext = *reinterpret_cast<const uint2 *>(act_in + i * COG_ACTION_BYTES);
   load_env(s, i, S);
   uint32_t srng = SRC == MASK_EXTERNAL ? 0u : rngs[i];
   regs_env(R, S);
@@ -2413,9 +2417,9 @@ DEV bool env_step_lane(const DevState &s, size_t i, const uint8_t *act_in, uint3
   const int na = ag + 1 >= (int)R.n_players() ? 0 : ag + 1;
   load_players(s, i, ag, na, S);
   uint8_t act[5];
-  if (SRC == MASK_SELECTED) step_action<SRC>(R, act_in, i, srng, act);
+  if (SRC == MASK_SELECTED) step_action<SRC>(R, ext, srng, act);
   regs_players(R, S);
-  if (SRC != MASK_SELECTED) step_action<SRC>(R, act_in, i, srng, act);
+  if (SRC != MASK_SELECTED) step_action<SRC>(R, ext, srng, act);
   STAMP(s, 1);
   const bool was_done = R.done() != 0u;
   const bool finish = !was_done && step_regs(R, act, s, i, na PH_PASS);
@@ -2735,7 +2739,7 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s_glob, int steps, uin
       const int na = ag + 1 >= (int)R.n_players() ? 0 : ag + 1;   // at the end of the last step
       uint8_t act[5];
       PH(0);
-      if (SRC == MASK_SELECTED) step_action<SRC>(R, nullptr, i, srng, act);
+      if (SRC == MASK_SELECTED) step_action<SRC>(R, make_uint2(0u, 0u), srng, act);
 #ifdef COG_ABLATE_DUPSAMPLE                                // diagnostic timing builds only: the
       {                                                    // sampler's cost, measured by running
         uint32_t r2 = srng ^ 0x5555u;                      // it a second time on a discarded state
@@ -2745,7 +2749,7 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s_glob, int steps, uin
       }
 #endif
       regs_players(R, S);
-      if (SRC == MASK_STORED) step_action<SRC>(R, nullptr, i, srng, act);
+      if (SRC == MASK_STORED) step_action<SRC>(R, make_uint2(0u, 0u), srng, act);
       PH(1);
       const bool was_done = R.done() != 0u;
       const bool finish = !was_done && step_regs(R, act, s, i, na PH_PASS);
@@ -2996,7 +3000,7 @@ DEV void duo_stepper(DuoLds &D, const DevState &s_glob, int steps, uint32_t *__r
     bool ended = false, finish = false;
     uint8_t act[5];
     if (live) {
-      step_action<SRC>(R, nullptr, i, srng, act);
+      step_action<SRC>(R, make_uint2(0u, 0u), srng, act);
       const bool was_done = R.done() != 0u;
       finish = !was_done && step_regs(R, act, s, i, na PH_PASS);
       if (finish) R.set_done(1u);
