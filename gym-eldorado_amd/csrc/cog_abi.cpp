@@ -262,6 +262,10 @@ struct EnvShard {
   bool zc = false;
   uint8_t *h_obs_d = nullptr, *h_outs_d = nullptr, *mir = nullptr;
   bool mir_valid = false;
+  // the pinned views (tails and outs block) and the mirror equal HBM: set by every publish, cleared
+  // by any device work that no publish followed.  A host step then publishes directly
+  // (launch_step_pub), and pub_done tells finish() that the step already did.
+  bool host_synced = false, pub_done = false;
   Signal done;                        // completion word: word 32 of the shard's error line
 };
 
@@ -419,11 +423,18 @@ int enqueue_publish(EnvShard &k, const SamplerShard *q, uint8_t *h_act_d) {
 // smp (optional): a runner's sampler whose actions' host view is refreshed with the env's
 int finish(cog_env *e, bool refresh_host, cog_sampler *smp = nullptr) {
   const bool host = refresh_host && e->host;
-  for (EnvShard &k : e->sh) k.done.queued = false;        // (a failed call may have left one armed)
+  for (EnvShard &k : e->sh) {
+    if (!k.pub_done) k.done.queued = false;               // (a failed call may have left one armed)
+    k.host_synced = false;                                 // (until this call has published)
+  }
   for (size_t j = 0; j < e->sh.size(); j++) {
     EnvShard &k = e->sh[j];
     DeviceGuard g(k.device);
     int rc = COG_OK;
+    if (k.pub_done) {                                      // the step published itself
+      k.pub_done = false;
+      continue;
+    }
     if (host && k.zc) {
       const SamplerShard *q = smp ? &smp->sh[j] : nullptr;
       uint8_t *h_act = q ? const_cast<uint8_t *>(zc_device(smp->h_actions + q->first, q->n * COG_ACTION_BYTES)) : nullptr;
@@ -484,6 +495,7 @@ int finish(cog_env *e, bool refresh_host, cog_sampler *smp = nullptr) {
   }
   if (any_dirty && (rc = sync_all(e))) return rc;
   if (host) gather_small(e);
+  for (EnvShard &k : e->sh) k.host_synced = host && k.zc && k.mir_valid;
   return status_to_rc(flags, errors);
 }
 
@@ -670,7 +682,10 @@ int cog_env_shard_info(const cog_env *env, int k, size_t *first, size_t *count, 
 static int env_reset_impl(cog_env *e, const cog::ResetParams &p) {
   int rc = prepare_host(e);
   if (rc) return rc;
-  for (EnvShard &k : e->sh) k.done.queued = false;
+  for (EnvShard &k : e->sh) {
+    k.done.queued = false;
+    k.host_synced = false;                                 // (refresh_full: the mirror is rebuilt later)
+  }
   for (EnvShard &k : e->sh) {
     DeviceGuard g(k.device);
     if (cog::launch_reset(k.s, p, k.stream) || cog::launch_encode_all(k.s, k.stream))
@@ -744,6 +759,20 @@ int cog_env_step(cog_env *env, const cog_action_t *actions, size_t n) {
     if (!da || !zc_same_on(k.device, actions + k.first)) {                      // (and mapped alike on this GPU)
       HIPCHK(hipMemcpyAsync(k.d_actions, actions + k.first, k.n * COG_ACTION_BYTES, hipMemcpyHostToDevice, k.stream));
       da = k.d_actions;
+    }
+    uint32_t seq = 0, *ctr = nullptr;
+    k.pub_done = false;
+    if (env->host && k.zc && k.mir_valid && k.host_synced && cog::step_pub_ok(k.n) &&
+        (ctr = signal_arm(k.done, seq))) {                 // the step publishes and signals itself
+      cog::DevState ps = launch_state(k, true);
+      ps.pub_obs = k.h_obs_d;
+      ps.pub_outs = k.h_outs_d;
+      ps.pub_mir = k.mir;
+      if (cog::launch_step_pub(ps, da, k.stream, ctr, k.done.d, seq))
+        return fail(COG_ERR_HIP, std::string("step launch failed: ") + hipGetErrorString(hipGetLastError()));
+      signal_armed(k.done);
+      k.pub_done = true;
+      continue;
     }
     if (cog::launch_step(launch_state(k, env->host), da, k.stream))
       return fail(COG_ERR_HIP, std::string("step launch failed: ") + hipGetErrorString(hipGetLastError()));
@@ -1159,6 +1188,7 @@ static int runner_launch_fused(cog_runner *r, int steps) {
   const int src = (r->flags & COG_RUNNER_STORED_MASKS) ? cog::MASK_STORED : cog::MASK_SELECTED;
   const bool host = runner_host(r);
   int rc;
+  for (EnvShard &k : r->env->sh) k.host_synced = false;  // (device work: views stale until a publish)
   if (host && (rc = prepare_host(r->env))) return rc;
   for (size_t j = 0; j < r->env->sh.size(); j++) {
     EnvShard &k = r->env->sh[j];
@@ -1204,6 +1234,7 @@ int cog_runner_step(cog_runner *r) {
   const bool host = runner_host(r);
   int rc;
   if (host && (rc = prepare_host(r->env))) return rc;
+  for (EnvShard &k : r->env->sh) k.host_synced = false;
   for (size_t j = 0; j < r->env->sh.size(); j++) {
     EnvShard &k = r->env->sh[j];
     DeviceGuard g(k.device);

@@ -105,6 +105,9 @@ struct DevState {
   unsigned long long *stamps;        // diagnostic builds (COG_STAMPS) only: per-wave phase clocks
   uint32_t *park;                    // [n] rollout park codes: the step at which an env's episode
                                      // ended inside a launch (~0u: none), read by the fix-up kernel
+  // direct publish (launch_step_pub only; null otherwise): device addresses of the shard's pinned
+  // ObsData view and outs block, and the publish mirror (k_publish's `mir`)
+  uint8_t *pub_obs, *pub_outs, *pub_mir;
 };
 
 struct ResetParams {
@@ -121,6 +124,15 @@ int launch_init(const DevState &s, const uint32_t *seeds_host_unused, uint32_t d
 int launch_reset(const DevState &s, const ResetParams &p, void *stream);
 int launch_encode_all(const DevState &s, void *stream, int variant = 0);
 int launch_step(const DevState &s, const uint8_t *d_actions, void *stream);
+// a host-visible step whose pinned views equal the records in HBM (after a publish, no device-only
+// work since): every changed granule of a host-visible record is stored into the view and the
+// publish mirror by the step itself (s.pub_* set), envs whose episode ended are published by
+// comparison, and the last workgroup copies the status granules and stores the completion word
+// (sig_ctr: a zeroed device counter).  Returns -1 when the batch is too large for it
+// (step_pub_ok).
+int launch_step_pub(const DevState &s, const uint8_t *d_actions, void *stream, uint32_t *sig_ctr, uint32_t *sig_word,
+                    uint32_t seq);
+bool step_pub_ok(size_t n);
 // h_actions: device-mapped host view (or null); sig_ctr (or null), sig_word, seq: the in-kernel
 // completion word (the last workgroup stores seq into *sig_word; sig_ctr a zeroed device counter)
 int launch_sample(size_t n, const uint8_t *d_masks, uint32_t *d_rng, uint8_t *d_actions,

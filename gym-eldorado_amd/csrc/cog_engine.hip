@@ -2285,6 +2285,33 @@ DEV void regs_players(RegEnv &R, const Snap &S) {
     R.d[4 * k] = S.dk[k].x; R.d[4 * k + 1] = S.dk[k].y; R.d[4 * k + 2] = S.dk[k].z; R.d[4 * k + 3] = S.dk[k].w;
   }
 }
+// ObsData record granules, and the dynamic tail (phase, resources, shop, decks, stored masks) the
+// host views refresh: granules kTail0 .. kRecG - 1
+constexpr size_t kRecG = COG_OBS_BYTES / 16, kTail0 = COG_OBS_MAP_BYTES / 16, kTailG = kRecG - kTail0;
+
+// Direct publish (k_env_step_pub): a store of a host-visible record also goes to the pinned view
+// and to the publish mirror (k_publish's `mir`: [n][kTailG] tail granules, then the outs block),
+// which keeps both equal to HBM without a compare pass.  PUB: 0 off, 1 an ObsData tail record of
+// env i, 2 a record of the outs block (status | selected masks | infos | rewards | dones | agents).
+template <int PUB, class T>
+DEV void pub_store(const DevState &s, size_t i, T *dev, const T &v) {
+  *dev = v;
+  if (PUB == 1) {
+    const size_t off = (size_t)(reinterpret_cast<const uint8_t *>(dev) - s.obs);
+    *reinterpret_cast<T *>(s.pub_obs + off) = v;
+    *reinterpret_cast<T *>(s.pub_mir + i * (kTailG * 16) + (off - i * COG_OBS_BYTES - COG_OBS_MAP_BYTES)) = v;
+  } else if (PUB == 2) {
+    const size_t off = (size_t)(reinterpret_cast<const uint8_t *>(dev) - reinterpret_cast<const uint8_t *>(s.status));
+    *reinterpret_cast<T *>(s.pub_outs + off) = v;
+    *reinterpret_cast<T *>(s.pub_mir + s.n * (kTailG * 16) + off) = v;
+  }
+}
+template <int PUB = 0>
+DEV void store_mask_record(const DevState &s, size_t i, uint4 *rec, const MBits &b, uint32_t gm) {
+#pragma unroll
+  for (int g = 0; g < 6; g++)
+    if ((gm >> g) & 1u) pub_store<PUB>(s, i, rec + g, mask_granule(b, g));
+}
 DEV void store_mask_record(uint4 *rec, const MBits &b, uint32_t gm) {
 #pragma unroll
   for (int g = 0; g < 6; g++)
@@ -2296,26 +2323,30 @@ DEV void store_mask_record(uint4 *rec, const MBits &b, uint32_t gm) {
 // mask bit vectors) is stored by the single-step kernel on every step; the rollout keeps it
 // on-chip and stores it before anything reads it back (episode end, reset, end of launch).
 // A move stores the new locations at once: the next move re-reads them.
+template <bool PUB = false>
 DEV void store_outputs(const DevState &s, size_t i, int ag, int na, const Snap &S, const RegEnv &R) {
+  constexpr int PT = PUB ? 1 : 0, PO = PUB ? 2 : 0;        // (direct publish: tail / outs records)
   uint8_t *ob = s.obs + i * COG_OBS_BYTES;
-  s.info[i * COG_INFO_BYTES + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag] = (uint8_t)(R.info_steps >> (8 * ag));
+  pub_store<PO>(s, i, s.info + i * COG_INFO_BYTES + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag,
+                (uint8_t)(R.info_steps >> (8 * ag)));
   if (R.moved) reinterpret_cast<uint4 *>(s.priv + i)[2] = R.g2;
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     const uint4 v = make_uint4(R.sh[4 * k], R.sh[4 * k + 1], R.sh[4 * k + 2], R.sh[4 * k + 3]);
-    if (ne4(v, S.sh[k])) reinterpret_cast<uint4 *>(ob + COG_OBS_PHASE)[k] = v;
+    if (ne4(v, S.sh[k])) pub_store<PT>(s, i, reinterpret_cast<uint4 *>(ob + COG_OBS_PHASE) + k, v);
   }
   uint8_t *deck = deck_ptr(s, i, ag);
 #pragma unroll
   for (int k = 0; k < 7; k++) {
     const uint4 v = make_uint4(R.d[4 * k], R.d[4 * k + 1], R.d[4 * k + 2], R.d[4 * k + 3]);
-    if (ne4(v, S.dk[k])) reinterpret_cast<uint4 *>(deck)[k] = v;
+    if (ne4(v, S.dk[k])) pub_store<PT>(s, i, reinterpret_cast<uint4 *>(deck) + k, v);
   }
   const MBits bs = bits_of(R.sel), ba = bits_of(R.sta), bn = bits_of(R.stn);
-  store_mask_record(reinterpret_cast<uint4 *>(s.sel + i * COG_MASK_BYTES), bs, mask_diff_granules(bs, S.sel));
-  store_mask_record(reinterpret_cast<uint4 *>(deck + COG_PD_MASK), ba, mask_diff_granules(ba, S.sta));
+  store_mask_record<PO>(s, i, reinterpret_cast<uint4 *>(s.sel + i * COG_MASK_BYTES), bs, mask_diff_granules(bs, S.sel));
+  store_mask_record<PT>(s, i, reinterpret_cast<uint4 *>(deck + COG_PD_MASK), ba, mask_diff_granules(ba, S.sta));
   if (na != ag)
-    store_mask_record(reinterpret_cast<uint4 *>(deck_ptr(s, i, na) + COG_PD_MASK), bn, mask_diff_granules(bn, S.stn));
+    store_mask_record<PT>(s, i, reinterpret_cast<uint4 *>(deck_ptr(s, i, na) + COG_PD_MASK), bn,
+                          mask_diff_granules(bn, S.stn));
 }
 DEV void store_private(const DevState &s, size_t i, int ag, int na, const Snap &S, const RegEnv &R) {
   uint4 *pw = reinterpret_cast<uint4 *>(s.priv + i);
@@ -2331,8 +2362,9 @@ DEV void store_private(const DevState &s, size_t i, int ag, int na, const Snap &
   if (mask_diff_granules(ba, S.sta)) s.heads[5 * i + 1 + ag] = mbits_u4(ba);
   if (na != ag && mask_diff_granules(bn, S.stn)) s.heads[5 * i + 1 + na] = mbits_u4(bn);
 }
+template <bool PUB = false>
 DEV void store_changes(const DevState &s, size_t i, int ag, int na, const Snap &S, const RegEnv &R) {
-  store_outputs(s, i, ag, na, S, R);
+  store_outputs<PUB>(s, i, ag, na, S, R);
   store_private(s, i, ag, na, S, R);
 }
 
@@ -2362,16 +2394,18 @@ DEV void step_action(RegEnv &R, const uint2 &ext, uint32_t &srng, uint8_t act[5]
 // auto-resets, and end_of_step_b then completes the reset (true: the map was regenerated, the
 // wave encodes it).  `out` caches (dones[i] | agent_selection[i] << 8) as last stored (~0u:
 // unknown), so bytes that already hold the value are not stored again.
+template <bool PUB = false>
 DEV bool end_of_step_a(const DevState &s, size_t i, bool was_done, bool finish, uint32_t &agent, uint32_t &out) {
+  constexpr int PO = PUB ? 2 : 0;                          // (an ended episode: pub_env_compare)
   if (finish) finish_episode(make_ctx(s, i));
   const bool done = was_done || finish;
-  if ((out & 0xffu) != (done ? 1u : 0u)) s.done[i] = done ? 1 : 0;   // dones[i] before the auto-reset
-  if (done && s.autoreset) {
+  if ((out & 0xffu) != (done ? 1u : 0u)) pub_store<PO>(s, i, s.done + i, (uint8_t)(done ? 1 : 0));   // dones[i]
+  if (done && s.autoreset) {                                                                        // before the reset
     env_reset_pre(make_ctx(s, i));
     out = (out & ~0xffu) | 1u;
     return true;
   }
-  if (((out >> 8) & 0xffu) != (agent & 0xffu)) s.agent[i] = (uint8_t)agent;
+  if (((out >> 8) & 0xffu) != (agent & 0xffu)) pub_store<PO>(s, i, s.agent + i, (uint8_t)agent);
   out = (done ? 1u : 0u) | (agent & 0xffu) << 8;
   return false;
 }
@@ -2398,9 +2432,9 @@ DEV bool end_of_step_b(const DevState &s, size_t i, bool gen_ok, uint32_t &agent
 
 // One step of env i: load (two rounds; the sampler runs on round 1 while round 2 is in
 // flight), step on registers, store what changed, [finish / auto-reset].
-template <int SRC>
+template <int SRC, bool PUB = false>
 DEV bool env_step_lane(const DevState &s, size_t i, const uint8_t *act_in, uint32_t *rngs, uint8_t *actions_out,
-                       const UidEntry *tab, uint32_t &agent, uint32_t &out) {
+                       const UidEntry *tab, uint32_t &agent, uint32_t &out, bool *ended = nullptr) {
   STAMP(s, 0);
   PH_DECL;
   Snap S;
@@ -2425,7 +2459,8 @@ DEV bool env_step_lane(const DevState &s, size_t i, const uint8_t *act_in, uint3
   const bool finish = !was_done && step_regs(R, act, s, i, na PH_PASS);
   if (finish) R.set_done(1u);
   STAMP(s, 2);
-  store_changes(s, i, ag, na, S, R);
+  store_changes<PUB>(s, i, ag, na, S, R);
+  if (ended) *ended = was_done || finish;
   if (SRC != MASK_EXTERNAL) {                              // (every store after the step's loads)
     rngs[i] = srng;
     store_action(actions_out + i * COG_ACTION_BYTES, act);
@@ -2433,7 +2468,7 @@ DEV bool env_step_lane(const DevState &s, size_t i, const uint8_t *act_in, uint3
   STAMP(s, 3);
   agent = R.agent();
   out = ~0u;
-  const bool rs = end_of_step_a(s, i, was_done, finish, agent, out);
+  const bool rs = end_of_step_a<PUB>(s, i, was_done, finish, agent, out);
   STAMP(s, 4);
   return rs;                                               // the env auto-resets (end_of_step_b)
 }
@@ -2452,6 +2487,105 @@ __global__ void __launch_bounds__(64) k_env_step(DevState s, const uint8_t *__re
   if (rs) enc = end_of_step_b(s, i, ok, agent, out);
   wave_encode(s, i, enc);                                  // converged: the whole wave encodes
   STAMP(s, 5);
+}
+
+// In-kernel completion word of a host call (the host spins on it, cog_abi.cpp Signal): the last
+// workgroup to finish stores `seq` into the pinned word, after every workgroup's stores (device
+// records and the host views) have been acknowledged.  A counter in device memory finds the last
+// workgroup (about 14 ns per arriving workgroup on one address, tools/latprobe.hip), so kernels
+// that signal keep their grids small; the last workgroup re-arms the counter.
+struct GridSignal {
+  uint32_t *ctr;                      // device counter (0 between calls); null: no signal
+  uint32_t *word;                     // device address of the pinned host word
+  uint32_t seq;
+};
+DEV void grid_signal(const GridSignal &g) {
+  if (!g.ctr) return;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();                                       // this workgroup's stores performed
+    if (atomicAdd(g.ctr, 1u) == gridDim.x - 1) {
+      __hip_atomic_store(g.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(g.word, g.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// Direct publish of an env whose episode ended in this step (finish_episode, dones, reset and
+// encode rewrote records the step's own stores do not cover): its ObsData tail and its records in
+// the outs block compared granule by granule with the mirror, as k_publish does, by the env's lane.
+DEV void pub_compare(const DevState &s, const uint4 *src, uint4 *mir, uint4 *dst, int ng) {
+  for (int g0 = 0; g0 < ng; g0 += 8) {                     // 8 granules in flight per round
+    uint4 c[8], m[8];
+#pragma unroll
+    for (int g = 0; g < 8; g++)
+      if (g0 + g < ng) {
+        c[g] = src[g0 + g];
+        m[g] = mir[g0 + g];
+      }
+#pragma unroll
+    for (int g = 0; g < 8; g++)
+      if (g0 + g < ng && ne4(c[g], m[g])) {
+        dst[g0 + g] = c[g];
+        mir[g0 + g] = c[g];
+      }
+  }
+}
+DEV void pub_env_compare(const DevState &s, size_t i) {
+  const size_t mo = s.n * kTailG;                          // the outs block in the mirror (granules)
+  uint4 *mir = reinterpret_cast<uint4 *>(s.pub_mir);
+  const uint4 *obs = reinterpret_cast<const uint4 *>(s.obs) + i * kRecG + kTail0;
+  pub_compare(s, obs, mir + i * kTailG, reinterpret_cast<uint4 *>(s.pub_obs) + i * kRecG + kTail0, (int)kTailG);
+  const uint4 *outs = reinterpret_cast<const uint4 *>(s.status);
+  uint4 *hout = reinterpret_cast<uint4 *>(s.pub_outs);
+  const size_t sel = (size_t)(s.sel - reinterpret_cast<const uint8_t *>(s.status)) / 16 + i * (COG_MASK_BYTES / 16);
+  const size_t inf = (size_t)(s.info - reinterpret_cast<const uint8_t *>(s.status)) / 16 + i * (COG_INFO_BYTES / 16);
+  const size_t rew = (size_t)(reinterpret_cast<const uint8_t *>(s.rew) - reinterpret_cast<const uint8_t *>(s.status)) / 16 + i;
+  pub_compare(s, outs + sel, mir + mo + sel, hout + sel, COG_MASK_BYTES / 16);
+  pub_compare(s, outs + inf, mir + mo + inf, hout + inf, COG_INFO_BYTES / 16);
+  pub_compare(s, outs + rew, mir + mo + rew, hout + rew, 1);
+  pub_store<2>(s, i, s.done + i, s.done[i]);               // (bytes: stored as they are)
+  pub_store<2>(s, i, s.agent + i, s.agent[i]);
+}
+// k_env_step for a host-visible step whose pinned views equal HBM (launch_step_pub): the step's
+// stores go to the views and the mirror as well, ended episodes are published by comparison, and
+// the last workgroup copies the status granules (error flags, dirty-map count) and stores the
+// completion word -- one kernel instead of k_env_step + k_publish.
+__global__ void __launch_bounds__(64) k_env_step_pub(DevState s, const uint8_t *__restrict__ act_in, GridSignal sig) {
+  __shared__ UidEntry tab[kUidTab];
+  uid_tab_fill(tab);
+  const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t i = i0 < s.n ? i0 : 0;
+  bool rs = false, enc = false, ended = false;
+  uint32_t agent = 0, out = ~0u;
+  if (i0 < s.n) rs = env_step_lane<MASK_EXTERNAL, true>(s, i, act_in, nullptr, nullptr, tab, agent, out, &ended);
+  const bool ok = wave_generate(s, i, rs);                 // converged: the whole wave generates
+  if (rs) enc = end_of_step_b(s, i, ok, agent, out);
+  wave_encode(s, i, enc);                                  // converged: the whole wave encodes
+  if (__builtin_amdgcn_ballot_w64(ended)) {                // (wave-uniform) the wave's records as
+    __builtin_amdgcn_s_waitcnt(0);                         // stored, including other lanes' encode
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    if (ended) pub_env_compare(s, i);
+  }
+  // completion: the last workgroup to arrive publishes the status granules, then the word
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (__hip_atomic_fetch_add(sig.ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+      __hip_atomic_store(sig.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const uint4 *st = reinterpret_cast<const uint4 *>(s.status);
+      uint4 *mo = reinterpret_cast<uint4 *>(s.pub_mir) + s.n * kTailG;
+#pragma unroll
+      for (int g = 0; g < 4; g++) {
+        const uint4 v = st[g];
+        reinterpret_cast<uint4 *>(s.pub_outs)[g] = v;
+        mo[g] = v;
+      }
+      __threadfence();
+      __hip_atomic_store(sig.word, sig.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 // Persistent rollout: K x (sample; step) per launch (the runner's device loop, runner.h:46-55).
@@ -3233,28 +3367,6 @@ __global__ void __launch_bounds__(64) k_env_fixup(DevState s, int steps, uint32_
   }
 }
 
-// In-kernel completion word of a host call (the host spins on it, cog_abi.cpp Signal): the last
-// workgroup to finish stores `seq` into the pinned word, after every workgroup's stores (device
-// records and the host views) have been acknowledged.  A counter in device memory finds the last
-// workgroup (about 14 ns per arriving workgroup on one address, tools/latprobe.hip), so kernels
-// that signal keep their grids small; the last workgroup re-arms the counter.
-struct GridSignal {
-  uint32_t *ctr;                      // device counter (0 between calls); null: no signal
-  uint32_t *word;                     // device address of the pinned host word
-  uint32_t seq;
-};
-DEV void grid_signal(const GridSignal &g) {
-  if (!g.ctr) return;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();                                       // this workgroup's stores performed
-    if (atomicAdd(g.ctr, 1u) == gridDim.x - 1) {
-      __hip_atomic_store(g.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(g.word, g.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-}
-
 // masks may be device memory or pinned host memory (zero-copy); h_actions (may be null) is the
 // host view of the actions, written straight over PCIe beside the device copy
 __global__ void __launch_bounds__(256) k_sample(size_t n, const uint8_t *__restrict__ masks,
@@ -3285,7 +3397,6 @@ __global__ void __launch_bounds__(256) k_sample(size_t n, const uint8_t *__restr
 // depending on the box).  force = 1 stores everything (the host views' state is unknown).  The
 // sampler's actions (the 8 bytes store_action writes at the head of each 64-B record) ride along
 // when act is given.
-constexpr size_t kRecG = COG_OBS_BYTES / 16, kTail0 = COG_OBS_MAP_BYTES / 16, kTailG = kRecG - kTail0;
 // Two granules per work-item, both loaded before either is compared (all loads in flight), so
 // that a small batch's grid is small enough for the in-kernel completion word (<= 128 workgroups:
 // 256 envs take 46); larger grids are signalled by k_signal after the kernel.
@@ -3440,6 +3551,15 @@ int launch_step(const DevState &s, const uint8_t *d_actions, void *stream) {
   if (!s.n) return 0;
   hipLaunchKernelGGL(k_env_step<MASK_EXTERNAL>, dim3(blocks_for(s.n, 64)), dim3(64), 0, (hipStream_t)stream, s,
                      d_actions, nullptr, nullptr);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+constexpr unsigned kStepPubMaxBlocks = 128;              // (completion counter arrivals)
+bool step_pub_ok(size_t n) { return n && blocks_for(n, 64) <= kStepPubMaxBlocks; }
+int launch_step_pub(const DevState &s, const uint8_t *d_actions, void *stream, uint32_t *sig_ctr, uint32_t *sig_word,
+                    uint32_t seq) {
+  if (!step_pub_ok(s.n) || !sig_ctr || !s.pub_obs || !s.pub_outs || !s.pub_mir) return -1;
+  hipLaunchKernelGGL(k_env_step_pub, dim3(blocks_for(s.n, 64)), dim3(64), 0, (hipStream_t)stream, s, d_actions,
+                     GridSignal{sig_ctr, sig_word, seq});
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_sample(size_t n, const uint8_t *d_masks, uint32_t *d_rng, uint8_t *d_actions, void *stream,
