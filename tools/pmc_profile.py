@@ -7,7 +7,7 @@ stamped with the hash of the engine source so that bench.py uses it only for the
 it measures.
 
     python tools/pmc_profile.py <dir of the K-step capture>:<K> [<dir>:<K> ...]  [--envs 65536]
-                                [--coeff <tools/store_coeff.sh output dir>]
+                                [--coeff <tools/store_coeff.sh output dir> | --coeff keep]
 
 The first capture gives the per-wave-step instruction and cycle counts (use a long K); every
 capture gives the rollout's HBM bytes and L2 write hits / misses per launch at its K.  --coeff adds
@@ -114,7 +114,12 @@ def main(specs, envs=65536, coeff=None):
                                                        "misses": kk["TCC_MISS_sum"],
                                                        "fabric_write_requests": kk.get("TCC_EA0_WRREQ_sum")}
     out["k_env_rollout"] = ro
-    if coeff:
+    if coeff == "keep":                     # the store costs are the probe's, not the engine's: carry them over
+        with open(os.path.join(ROOT, "profiles", "pmc_profile.json")) as f:
+            prev = json.load(f).get("store_costs")
+        if prev:
+            out["store_costs"] = prev
+    elif coeff:
         out["store_costs"] = store_costs(coeff)
     with open(os.path.join(ROOT, "profiles", "pmc_profile.json"), "w") as f:
         json.dump(out, f, indent=1)
