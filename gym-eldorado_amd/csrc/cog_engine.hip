@@ -2856,6 +2856,7 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s_glob, int steps, uin
   // merged with them, so the wait-count pass places no per-iteration vmcnt wait for registers
   // they wrote (such a wait, executed every step, would also wait for the step's stores).
   __builtin_amdgcn_s_waitcnt(0);
+  if (PIPE && !FIX) __syncthreads();                       // the decks in LDS: the storing wave's image
   PH_DECL;
   for (int t = FIX ? 1 : 0; t < steps; t++) {
     if (PIPE) {                                            // every lane, every step: the records
@@ -3002,7 +3003,13 @@ __global__ void __launch_bounds__(128) k_env_rollout_pipe(DevState s, int steps,
     const DevState v = wave_view(s, base);
     uint8_t *av = actions_out + base * COG_ACTION_BYTES;
     DeckImage I;
-    if (l < ne) deck_image_load(I, v, (size_t)l);
+    __syncthreads();                                       // the stepping wave's fill is in LDS: the
+    if (l < ne) {                                          // image from there, not a second read of
+#pragma unroll                                             // every deck from memory
+      for (int p = 0; p < 4; p++)
+#pragma unroll
+        for (int k = 0; k < 7; k++) I.d[p][k] = L.deck[p][k][l];
+    }
     for (int t = 0; t < steps; t++) {
       __syncthreads();
       if (l < ne) out_record_store(O, t & 1, l, v, (size_t)l, av, I);
@@ -3034,6 +3041,9 @@ __global__ void __launch_bounds__(128) k_env_rollout_pipe(DevState s, int steps,
 // acts after a turn change (`slot`: the next player's deck as of the step's start -- only the
 // acting player's deck changes within a step).
 //
+// Before the loop, barrier B: the storing wave has loaded every player's deck (its image) and
+// hands the acting player's to the stepping wave through the ring's deck buffer 1, so the stepping
+// wave's prologue is one round of loads (no dependent read of the deck the agent selects).
 // Per step t, two barriers (both waves execute them):
 //   stepping wave: step t on registers; pl/cells/heads of the acting player to LDS;
 //                  X_t; record t to the ring; on a turn change the next player's records from
@@ -3113,12 +3123,6 @@ DEV void duo_stepper(DuoLds &D, const DevState &s_glob, int steps, uint32_t *__r
     srng = rngs[i];
     ag = (int)R.agent();
     na = (int)next_player((uint32_t)ag, R.n_players());
-    const uint4 *dk = reinterpret_cast<const uint4 *>(deck_ptr(s, i, ag));
-#pragma unroll
-    for (int k = 0; k < 7; k++) {
-      const uint4 v = dk[k];
-      R.d[4 * k] = v.x; R.d[4 * k + 1] = v.y; R.d[4 * k + 2] = v.z; R.d[4 * k + 3] = v.w;
-    }
     R.P = unpack_player(D.pl[ag][l]);
     R.na_active = (D.pl[na][l].y >> 16) & 0xffu;
     R.cells_a = D.cells[ag][l];
@@ -3129,6 +3133,14 @@ DEV void duo_stepper(DuoLds &D, const DevState &s_glob, int steps, uint32_t *__r
   R.tab = D.tab;
   // every load above completes before the loop (no per-iteration vmcnt wait covers them)
   __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();                                         // B: the storing wave loaded every deck;
+  if (live) {                                              // the acting player's from its hand-over
+#pragma unroll                                             // (no second, dependent read of memory)
+    for (int k = 0; k < 7; k++) {
+      const uint4 v = D.deckr[1][k][l];
+      R.d[4 * k] = v.x; R.d[4 * k + 1] = v.y; R.d[4 * k + 2] = v.z; R.d[4 * k + 3] = v.w;
+    }
+  }
   PH_DECL;
   for (int t = 0; t < steps; t++) {
     bool ended = false, finish = false;
@@ -3253,10 +3265,14 @@ DEV void duo_storer(DuoLds &D, const DevState &s_glob, int steps, uint8_t *__res
 #pragma unroll
     for (int p = 0; p < 4; p++) stb[p] = mbits_of(s.heads[5 * i + 1 + p]);
     const uint4 g1 = reinterpret_cast<const uint4 *>(s.priv + i)[1];
-    const int na0 = (int)next_player(g1.y & 0xffu, g1.x & 0xffu);
+    const int ag0 = (int)(g1.y & 0xffu), na0 = (int)next_player(g1.y & 0xffu, g1.x & 0xffu);
 #pragma unroll
-    for (int k = 0; k < 7; k++) D.slot[k][l] = sel4_of(I, na0, k);
+    for (int k = 0; k < 7; k++) {
+      D.slot[k][l] = sel4_of(I, na0, k);
+      D.deckr[1][k][l] = sel4_of(I, ag0, k);               // (buffer 1 is first written at step 1)
+    }
   }
+  __syncthreads();                                         // B: the acting player's deck handed over
   __syncthreads();                                         // X_0
   PH_DECL;
   for (int t = 0; t < steps; t++) {
