@@ -86,3 +86,51 @@ def test_host_loop_two_shards(cg):
     # one handle, two shards (both on GPU 0 here), ragged 150 + 151, with resets
     env, smp, orc, osm = make(cg, 301, 5150, cg.HARD, 30, device=[0, 0])
     host_steps(env, smp, orc, osm, 120, "two shards")
+
+
+SPIN_OFF_SCRIPT = r"""
+import hashlib, sys
+sys.path.insert(0, sys.argv[1])
+import city_of_gold as cg
+n, seed = 256, 31337
+env = cg.vec.get_vec_env(n)()
+smp = cg.vec.get_vec_sampler(n)(seed)
+env.reset(seed, 4, 3, cg.EASY, 25, False)
+masks, acts = env.selected_action_masks, smp.get_actions()
+h = hashlib.sha256()
+for _ in range(60):
+    smp.sample(masks)
+    env.step(acts)
+    for a in (acts, env.observations, env.selected_action_masks, env.infos, env.rewards, env.dones,
+              env.agent_selection):
+        h.update(a.tobytes())
+print(h.hexdigest())
+"""
+
+
+def test_completion_without_spin_same_bytes(cg, tmp_path):
+    """COG_SPIN_US=0 (every call ends on hipStreamSynchronize, as in round 2) gives the bytes the
+    default completion-word path gives, through the same host loop with episode ends."""
+    import hashlib
+    import os
+    import subprocess
+    import sys
+    pkg = os.path.dirname(os.path.dirname(cg.__file__))
+    n, seed = 256, 31337
+    env = cg.vec.get_vec_env(n)()
+    smp = cg.vec.get_vec_sampler(n)(seed)
+    env.reset(seed, 4, 3, cg.EASY, 25, False)
+    masks, acts = env.selected_action_masks, smp.get_actions()
+    h = hashlib.sha256()
+    for _ in range(60):
+        smp.sample(masks)
+        env.step(acts)
+        for a in (acts, env.observations, env.selected_action_masks, env.infos, env.rewards, env.dones,
+                  env.agent_selection):
+            h.update(a.tobytes())
+    script = tmp_path / "spin_off.py"
+    script.write_text(SPIN_OFF_SCRIPT)
+    run = subprocess.run([sys.executable, str(script), pkg], capture_output=True, text=True, timeout=150,
+                         env=dict(os.environ, COG_SPIN_US="0", COG_NO_TORCH="1"))
+    assert run.returncode == 0, run.stderr[-2000:]
+    assert run.stdout.strip().splitlines()[-1] == h.hexdigest()
