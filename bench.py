@@ -492,9 +492,14 @@ def main():
         enc_gbs = ENCODE_BYTES * n / (enc_ms / 1e3) / 1e9
         cp_torch = copy_peak_gbs(d)
         cp = cg._city_of_gold.time_copy(dev, 1 << 31, 5)
+        mix = cg._city_of_gold.time_stream_mix(dev, 1 << 28, 5)   # 256 MiB read, 1.75 GiB written
         extras["encode"] = {"kernel": "k_encode", "ms": enc_ms, "achieved": enc_gbs, "unit": "GB/s",
                             "frac": enc_gbs / HBM_PEAK_GBS, "copy_peak_GBs": cp,
                             "frac_of_copy_peak": enc_gbs / cp if cp else None,
+                            "mix_peak_GBs": mix, "frac_of_mix_peak": enc_gbs / mix if mix else None,
+                            "mix_peak_note": "a coalesced stream with the encode's read:write mix (16 B read, "
+                                             "112 B written per work-item), the faster of plain and "
+                                             "non-temporal stores: the peak of a kernel shaped like the encode",
                             "copy_peak_note": "the engine's copy kernel (16-B loads/stores, plain or non-temporal, 8 or 32 waves per CU: the fastest), "
                                               "2 x 2 GiB buffers, read + write bytes); torch's copy_ in the "
                                               "same run: %.0f GB/s" % cp_torch if cp_torch else "",

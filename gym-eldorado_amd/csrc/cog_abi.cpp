@@ -921,7 +921,14 @@ int cog_env_time_encode(cog_env *env, int iters, int variant, double *ms_per_lau
   return COG_OK;
 }
 
+static int time_copy_variants(int device, size_t bytes, int iters, double *gb_per_s, bool mix);
 int cog_time_copy(int device, size_t bytes, int iters, double *gb_per_s) {
+  return time_copy_variants(device, bytes, iters, gb_per_s, false);
+}
+int cog_time_stream_mix(int device, size_t bytes, int iters, double *gb_per_s) {
+  return time_copy_variants(device, bytes, iters, gb_per_s, true);
+}
+static int time_copy_variants(int device, size_t bytes, int iters, double *gb_per_s, bool mix) {
   if (iters < 1 || bytes < 16 || !gb_per_s) return fail(COG_ERR_INVALID, "bad argument");
   bytes &= ~(size_t)15;
   int cnt = 0;
@@ -931,12 +938,14 @@ int cog_time_copy(int device, size_t bytes, int iters, double *gb_per_s) {
   hipStream_t st = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   int rc = COG_OK;
-  if (hipMalloc(&a, bytes) != hipSuccess || hipMalloc(&b, bytes) != hipSuccess) rc = fail(COG_ERR_OOM, "copy buffers");
+  const size_t out_bytes = mix ? 7 * bytes : bytes;      // (mix: `bytes` read, 7x written)
+  if (hipMalloc(&a, bytes) != hipSuccess || hipMalloc(&b, out_bytes) != hipSuccess) rc = fail(COG_ERR_OOM, "copy buffers");
   if (!rc && (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
               hipEventCreate(&e1) != hipSuccess || hipMemsetAsync(a, 1, bytes, st) != hipSuccess))
     rc = fail(COG_ERR_HIP, "copy setup");
   double best = 0.0;
-  for (int v = 0; v < 8 && !rc; v++) {                    // the fastest of the eight variants
+  const int v0 = mix ? 8 : 0, v1 = mix ? 10 : 8;         // the fastest variant
+  for (int v = v0; v < v1 && !rc; v++) {
     if (cog::launch_copy_peak(a, b, bytes, st, v)) rc = fail(COG_ERR_HIP, "copy launch failed");   // warm-up
     if (rc) break;
     (void)hipEventRecord(e0, st);
@@ -946,7 +955,7 @@ int cog_time_copy(int device, size_t bytes, int iters, double *gb_per_s) {
     float ms = 0.f;
     if (!rc && (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess))
       rc = fail(COG_ERR_HIP, "copy timing");
-    if (!rc) best = std::max(best, 2.0 * (double)bytes * iters / ((double)ms * 1e-3) / 1e9);
+    if (!rc) best = std::max(best, (double)(bytes + out_bytes) * iters / ((double)ms * 1e-3) / 1e9);
   }
   if (!rc) *gb_per_s = best;
   if (st) (void)hipStreamSynchronize(st);

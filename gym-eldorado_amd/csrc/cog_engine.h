@@ -156,7 +156,8 @@ int launch_seed_sampler(size_t n, uint64_t seed, size_t first, uint32_t *d_rng, 
 // earlier packet of the stream has completed
 int launch_signal(uint32_t *d_word, uint32_t seq, void *stream);
 // variant bit 0: non-temporal loads/stores; bit 1: 32 waves per CU instead of 8 (grid stride);
-// bit 2: one pass, 32 KiB per workgroup (bit 1 ignored); bytes: a multiple of 16
+// bit 2: one pass, 32 KiB per workgroup (bit 1 ignored); bit 3: the encode's 1:7 read:write mix
+// (reads `bytes`, writes 7 x `bytes` into dst; bit 0 = non-temporal stores); bytes: a multiple of 16
 int launch_copy_peak(const void *src, void *dst, size_t bytes, void *stream, int variant);
 
 }  // namespace cog

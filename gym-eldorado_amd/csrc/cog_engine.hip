@@ -3528,6 +3528,18 @@ __global__ void __launch_bounds__(256) k_copy_block(const u32x4_t *__restrict__ 
   }
 }
 
+// The encode's own read:write mix as a stream (1 granule read, 7 written, all coalesced): the
+// bandwidth an HBM-bound kernel of that mix can reach on this chip, the peak k_encode (16 B of
+// cells read, 112 B of observation written per work-item) is compared with.
+template <bool NT>
+__global__ void __launch_bounds__(256) k_stream_mix(const u32x4_t *__restrict__ src, u32x4_t *__restrict__ dst, size_t n_rd) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_rd) return;
+  const u32x4_t v = cp_ld<false>(src + i);
+#pragma unroll
+  for (int k = 0; k < 7; k++) cp_st<NT>(v + (unsigned)k, dst + i + (size_t)k * n_rd);
+}
+
 // ------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------
@@ -3679,6 +3691,12 @@ int launch_copy_peak(const void *src, void *dst, size_t bytes, void *stream, int
   const u32x4_t *a = static_cast<const u32x4_t *>(src);
   u32x4_t *b = static_cast<u32x4_t *>(dst);
   const size_t n16 = bytes / 16;
+  if (variant & 8) {                                  // the encode's mix: bytes / 16 granules read, 7x written
+    const dim3 g(blocks_for(n16, 256)), t(256);
+    if (variant & 1) hipLaunchKernelGGL(k_stream_mix<true>, g, t, 0, (hipStream_t)stream, a, b, n16);
+    else hipLaunchKernelGGL(k_stream_mix<false>, g, t, 0, (hipStream_t)stream, a, b, n16);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   if (variant & 4) {                                  // one pass, 32 KiB per workgroup
     const dim3 g(blocks_for(n16, 2048)), t(256);
     if (variant & 1) hipLaunchKernelGGL(k_copy_block<true>, g, t, 0, (hipStream_t)stream, a, b, n16);

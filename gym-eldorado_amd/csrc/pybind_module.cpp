@@ -341,6 +341,15 @@ PYBIND11_MODULE(_city_of_gold, m) {
       },
       "device"_a = 0, "bytes"_a = (size_t)1 << 31, "iters"_a = 5,
       "read + write GB/s of the engine's device copy kernel (measurement)");
+  m.def(
+      "time_stream_mix",
+      [](int device, size_t bytes, int iters) {
+        double gbs = 0.0;
+        check(cog_time_stream_mix(device, bytes, iters, &gbs));
+        return gbs;
+      },
+      "device"_a = 0, "bytes"_a = (size_t)1 << 28, "iters"_a = 5,
+      "read + write GB/s of a stream with the encode's 1:7 read:write mix (measurement)");
 
   py::class_<VecEnv>(m, "VecEnvBase", py::dynamic_attr())
       .def(py::init<size_t, const py::object &>(), "n_envs"_a, "device"_a = py::none())

@@ -151,6 +151,10 @@ COG_API int cog_env_time_encode(cog_env *env, int iters, int variant, double *ms
  * `device`: the copy peak beside which the encode's HBM fraction is reported (BASELINE.md "a
  * measured copy-kernel peak") */
 COG_API int cog_time_copy(int device, size_t bytes, int iters, double *gb_per_s);
+/* measurement: read + write bytes per second of a stream with the encode's read:write mix (reads
+ * `bytes`, writes 7 x `bytes`, coalesced, plain or non-temporal stores: the faster) on `device`:
+ * the bandwidth peak of a kernel shaped like the map-observation encode */
+COG_API int cog_time_stream_mix(int device, size_t bytes, int iters, double *gb_per_s);
 COG_API int cog_env_device(const cog_env *env); /* device ordinal */
 /* on (default): a finished env is reset inside the same step call, as vec_cog_env<N>::step does
  * (vec_environment.h:56-59).  off: cog_env::step semantics (environment.cpp:91-95) -- the env
