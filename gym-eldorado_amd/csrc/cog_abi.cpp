@@ -1174,6 +1174,10 @@ static int runner_flush_sample(cog_runner *r) {
   for (size_t j = 0; j < r->env->sh.size(); j++) {
     EnvShard &k = r->env->sh[j];
     DeviceGuard g(k.device);
+    if (k.pub_done) {                                      // the actions' view needs the next publish
+      k.pub_done = false;
+      k.done.queued = false;
+    }
     int rc = sampler_run(r->smp->sh[j], r->smp->h_actions, k.s.sel, k.stream, false);
     if (rc) return rc;
   }
@@ -1193,16 +1197,41 @@ static int runner_timing_event(cog_runner *r, size_t j) {
 // `steps` fused sample+step launches on every shard; with timing on, one event pair per shard
 // brackets the batch (device time per launch = pair time / steps, the quantity rocprofv3's
 // kernel trace averages, without per-launch event overhead)
+// A shard's host-visible work that is not a direct publish: the views are stale until the next
+// publish, and a completion word armed by an earlier direct step no longer covers the stream.
+static void views_pending(EnvShard &k) {
+  k.host_synced = false;
+  k.pub_done = false;
+  k.done.queued = false;
+}
+
 static int runner_launch_fused(cog_runner *r, int steps) {
   const int src = (r->flags & COG_RUNNER_STORED_MASKS) ? cog::MASK_STORED : cog::MASK_SELECTED;
   const bool host = runner_host(r);
   int rc;
-  for (EnvShard &k : r->env->sh) k.host_synced = false;  // (device work: views stale until a publish)
   if (host && (rc = prepare_host(r->env))) return rc;
   for (size_t j = 0; j < r->env->sh.size(); j++) {
     EnvShard &k = r->env->sh[j];
     SamplerShard &q = r->smp->sh[j];
     DeviceGuard g(k.device);
+    // one host-visible step with the views in sync (runner.sample(); runner.step()): the step
+    // publishes itself, the sampled actions included (k_env_step_pub), as env.step() does
+    if (host && steps == 1 && !r->timing && k.zc && k.mir_valid && k.host_synced && cog::step_pub_ok(k.n) && q.n) {
+      uint8_t *h_act = const_cast<uint8_t *>(zc_device(r->smp->h_actions + q.first, q.n * COG_ACTION_BYTES));
+      uint32_t seq = 0, *ctr = nullptr;
+      if (h_act && zc_same_on(k.device, r->smp->h_actions + q.first) && (ctr = signal_arm(k.done, seq))) {
+        cog::DevState ps = launch_state(k, true);
+        ps.pub_obs = k.h_obs_d;
+        ps.pub_outs = k.h_outs_d;
+        ps.pub_mir = k.mir;
+        if (cog::launch_sample_step_pub(ps, src, q.d_rng, q.d_actions, h_act, k.stream, ctr, k.done.d, seq))
+          return fail(COG_ERR_HIP, std::string("sample_step launch failed: ") + hipGetErrorString(hipGetLastError()));
+        signal_armed(k.done);
+        k.pub_done = true;                                 // (host_synced stays: the step keeps the views)
+        continue;
+      }
+    }
+    views_pending(k);                                      // (device work: views stale until a publish)
     if (r->timing) {
       if ((rc = runner_timing_event(r, j))) return rc;
       HIPCHK(hipEventRecord(r->ev[j][r->ev_used], k.stream));
@@ -1243,7 +1272,7 @@ int cog_runner_step(cog_runner *r) {
   const bool host = runner_host(r);
   int rc;
   if (host && (rc = prepare_host(r->env))) return rc;
-  for (EnvShard &k : r->env->sh) k.host_synced = false;
+  for (EnvShard &k : r->env->sh) views_pending(k);
   for (size_t j = 0; j < r->env->sh.size(); j++) {
     EnvShard &k = r->env->sh[j];
     DeviceGuard g(k.device);

@@ -133,6 +133,10 @@ int launch_step(const DevState &s, const uint8_t *d_actions, void *stream);
 int launch_step_pub(const DevState &s, const uint8_t *d_actions, void *stream, uint32_t *sig_ctr, uint32_t *sig_word,
                     uint32_t seq);
 bool step_pub_ok(size_t n);
+// the runner's fused sample + step in the same form; the sampled actions also go to the sampler's
+// pinned view (h_actions, device address)
+int launch_sample_step_pub(const DevState &s, int mask_source, uint32_t *d_rng, uint8_t *d_actions, uint8_t *h_actions,
+                           void *stream, uint32_t *sig_ctr, uint32_t *sig_word, uint32_t seq);
 // h_actions: device-mapped host view (or null); sig_ctr (or null), sig_word, seq: the in-kernel
 // completion word (the last workgroup stores seq into *sig_word; sig_ctr a zeroed device counter)
 int launch_sample(size_t n, const uint8_t *d_masks, uint32_t *d_rng, uint8_t *d_actions,

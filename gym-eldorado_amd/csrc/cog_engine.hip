@@ -2434,7 +2434,8 @@ DEV bool end_of_step_b(const DevState &s, size_t i, bool gen_ok, uint32_t &agent
 // flight), step on registers, store what changed, [finish / auto-reset].
 template <int SRC, bool PUB = false>
 DEV bool env_step_lane(const DevState &s, size_t i, const uint8_t *act_in, uint32_t *rngs, uint8_t *actions_out,
-                       const UidEntry *tab, uint32_t &agent, uint32_t &out, bool *ended = nullptr) {
+                       const UidEntry *tab, uint32_t &agent, uint32_t &out, bool *ended = nullptr,
+                       uint8_t *h_actions_out = nullptr) {
   STAMP(s, 0);
   PH_DECL;
   Snap S;
@@ -2464,6 +2465,7 @@ DEV bool env_step_lane(const DevState &s, size_t i, const uint8_t *act_in, uint3
   if (SRC != MASK_EXTERNAL) {                              // (every store after the step's loads)
     rngs[i] = srng;
     store_action(actions_out + i * COG_ACTION_BYTES, act);
+    if (PUB && h_actions_out) store_action(h_actions_out + i * COG_ACTION_BYTES, act);   // the sampler's view
   }
   STAMP(s, 3);
   agent = R.agent();
@@ -2551,14 +2553,20 @@ DEV void pub_env_compare(const DevState &s, size_t i) {
 // stores go to the views and the mirror as well, ended episodes are published by comparison, and
 // the last workgroup copies the status granules (error flags, dirty-map count) and stores the
 // completion word -- one kernel instead of k_env_step + k_publish.
-__global__ void __launch_bounds__(64) k_env_step_pub(DevState s, const uint8_t *__restrict__ act_in, GridSignal sig) {
+// SRC = MASK_EXTERNAL: env.step(actions); MASK_SELECTED / MASK_STORED: the runner's fused
+// sample + step, whose sampled actions also go to the sampler's pinned view (h_actions).
+template <int SRC>
+__global__ void __launch_bounds__(64) k_env_step_pub(DevState s, const uint8_t *__restrict__ act_in, uint32_t *__restrict__ rngs,
+                                                     uint8_t *__restrict__ actions_out, uint8_t *__restrict__ h_actions,
+                                                     GridSignal sig) {
   __shared__ UidEntry tab[kUidTab];
   uid_tab_fill(tab);
   const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t i = i0 < s.n ? i0 : 0;
   bool rs = false, enc = false, ended = false;
   uint32_t agent = 0, out = ~0u;
-  if (i0 < s.n) rs = env_step_lane<MASK_EXTERNAL, true>(s, i, act_in, nullptr, nullptr, tab, agent, out, &ended);
+  if (i0 < s.n)
+    rs = env_step_lane<SRC, true>(s, i, act_in, rngs, actions_out, tab, agent, out, &ended, h_actions);
   const bool ok = wave_generate(s, i, rs);                 // converged: the whole wave generates
   if (rs) enc = end_of_step_b(s, i, ok, agent, out);
   wave_encode(s, i, enc);                                  // converged: the whole wave encodes
@@ -3586,8 +3594,20 @@ bool step_pub_ok(size_t n) { return n && blocks_for(n, 64) <= kStepPubMaxBlocks;
 int launch_step_pub(const DevState &s, const uint8_t *d_actions, void *stream, uint32_t *sig_ctr, uint32_t *sig_word,
                     uint32_t seq) {
   if (!step_pub_ok(s.n) || !sig_ctr || !s.pub_obs || !s.pub_outs || !s.pub_mir) return -1;
-  hipLaunchKernelGGL(k_env_step_pub, dim3(blocks_for(s.n, 64)), dim3(64), 0, (hipStream_t)stream, s, d_actions,
-                     GridSignal{sig_ctr, sig_word, seq});
+  hipLaunchKernelGGL(k_env_step_pub<MASK_EXTERNAL>, dim3(blocks_for(s.n, 64)), dim3(64), 0, (hipStream_t)stream, s,
+                     d_actions, nullptr, nullptr, nullptr, GridSignal{sig_ctr, sig_word, seq});
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int launch_sample_step_pub(const DevState &s, int mask_source, uint32_t *d_rng, uint8_t *d_actions, uint8_t *h_actions,
+                           void *stream, uint32_t *sig_ctr, uint32_t *sig_word, uint32_t seq) {
+  if (!step_pub_ok(s.n) || !sig_ctr || !s.pub_obs || !s.pub_outs || !s.pub_mir || !h_actions) return -1;
+  const dim3 g(blocks_for(s.n, 64)), b(64);
+  if (mask_source == MASK_STORED)
+    hipLaunchKernelGGL(k_env_step_pub<MASK_STORED>, g, b, 0, (hipStream_t)stream, s, nullptr, d_rng, d_actions, h_actions,
+                       GridSignal{sig_ctr, sig_word, seq});
+  else
+    hipLaunchKernelGGL(k_env_step_pub<MASK_SELECTED>, g, b, 0, (hipStream_t)stream, s, nullptr, d_rng, d_actions,
+                       h_actions, GridSignal{sig_ctr, sig_word, seq});
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_sample(size_t n, const uint8_t *d_masks, uint32_t *d_rng, uint8_t *d_actions, void *stream,

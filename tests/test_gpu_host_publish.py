@@ -134,3 +134,45 @@ def test_completion_without_spin_same_bytes(cg, tmp_path):
                          env=dict(os.environ, COG_SPIN_US="0", COG_NO_TORCH="1"))
     assert run.returncode == 0, run.stderr[-2000:]
     assert run.stdout.strip().splitlines()[-1] == h.hexdigest()
+
+
+def test_runner_host_steps_publish_themselves(cg):
+    """runner.sample(); runner.step_sync() with host views (the C4 host loop) takes the direct
+    publish, sampled actions included; a sample() queued after a direct step, two steps before one
+    sync(), and env.step() between runner steps still leave every view as the reference's."""
+    n, seed = 512, 2024
+    env, smp, orc, osm = make(cg, n, seed, cg.MEDIUM, 30)
+    runner = cg.vec.get_runner(n)(env, smp, None)
+    acts = runner.get_actions()
+
+    def ref_step():
+        osm.sample(orc.selected_action_masks)
+        orc.step(osm.actions)
+
+    for t in range(60):                                    # the C4 loop, with episode ends
+        runner.sample()
+        runner.step_sync()
+        ref_step()
+        assert po.named_equal(acts, osm.actions) is None, f"runner loop: actions differ at step {t}"
+        assert_equal(env, orc, f"runner loop step {t}")
+    runner.sample()                                        # step, then a sample before the sync
+    runner.step()
+    runner.sample()
+    runner.sync()
+    ref_step()
+    osm.sample(orc.selected_action_masks)
+    assert po.named_equal(acts, osm.actions) is None, "the sample after a direct step is not in the view"
+    assert_equal(env, orc, "step + sample + sync")
+    runner.step()                                          # steps with those actions, then one more
+    orc.step(osm.actions)
+    runner.sample()
+    runner.step()
+    runner.sync()
+    ref_step()
+    assert_equal(env, orc, "two steps, one sync")
+    host_steps(env, smp, orc, osm, 5, "env.step between runner steps")
+    for t in range(5):
+        runner.sample()
+        runner.step_sync()
+        ref_step()
+        assert_equal(env, orc, f"runner after env.step, step {t}")
