@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstring>
 #include <functional>
 #include <vector>
 
@@ -92,7 +93,14 @@ static inline void spin(volatile unsigned *w, unsigned seq) {
   while (*w != seq) __builtin_ia32_pause();
 }
 
-int main() {
+int main(int argc, char **argv) {
+  // argv[1]: "spin" / "yield" / "block" -- hipSetDeviceFlags before the device is used (the host
+  // thread's wait in hipStreamSynchronize / hipDeviceSynchronize); default: the runtime's choice
+  if (argc > 1) {
+    const unsigned f = !strcmp(argv[1], "spin") ? hipDeviceScheduleSpin
+                       : !strcmp(argv[1], "yield") ? hipDeviceScheduleYield : hipDeviceScheduleBlockingSync;
+    printf("hipSetDeviceFlags(%s): %s\n", argv[1], hipGetErrorString(hipSetDeviceFlags(f)));
+  }
   hipStream_t st;
   if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return 1;
   unsigned *hword, *ctr;
