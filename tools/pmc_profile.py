@@ -24,7 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import pmc_summary  # noqa: E402
 
-ROLLOUT = "void cog::k_env_rollout<0, 64>"
+ROLLOUT = "void cog::k_env_rollout<0, 64"             # (prefix: <0, 64> or <0, 64, WPG>)
 STEP = "void cog::k_env_step<0>"
 ENCODE = "void cog::k_encode_lds<true>"
 
@@ -82,7 +82,7 @@ def main(specs, envs=65536, coeff=None):
         d, k = spec.rsplit(":", 1)
         k = int(k)
         res = summary(d)
-        r = res.get(ROLLOUT)
+        r = next((v for k, v in res.items() if k.startswith(ROLLOUT)), None)
         if r:
             b = traffic(r)
             if b is not None:
