@@ -50,6 +50,16 @@ def worker(rank, world, port, root, q):
     mine = rollout(hi - lo, shard_seed(SEED, lo), STEPS)
     gathered = [None] * world
     d.dist.all_gather_object(gathered, (lo, [x.hex() for x in mine]))
+    class _Runner:                                         # (no GPU: sync() stands in for the engine's)
+        calls = 0
+
+        def sync(self):
+            _Runner.calls += 1
+    r = _Runner()
+    d.barrier_sync(r)                                      # the bench's timed-region helpers
+    d.sync(r)
+    d.barrier()
+    assert _Runner.calls == 3
     mx = d.max(float(rank + 1))
     tot = d.sum(float(hi - lo))
     if rank == 0:
@@ -82,3 +92,21 @@ def test_shard_blocks():
     from city_of_gold.shard import shard
     assert [shard(10, r, 3) for r in range(3)] == [(0, 3), (3, 6), (6, 10)]
     assert sum(h - l for l, h in (shard(65536 * 8, r, 8) for r in range(8))) == 65536 * 8
+
+
+def test_bench_roofline_store_model():
+    """bench.roofline: the store bound from a profile's L2 hits / misses and the two store costs,
+    and the note (no frac) when the profile was measured at another size."""
+    import bench
+    n, k, launch = 65536, 20, 100e-6
+    prof = {"store_costs": {"c_hit_s": 5e-12, "c_miss_s": 16e-12},
+            "k_env_rollout": {"envs_per_launch": n, "valu_per_wave_step": 1000.0,
+                              "l2_per_launch": {"20": {"writes": 8.0e6, "hits": 4.5e6, "misses": 3.5e6}},
+                              "bytes_per_step_launch": {"20": 3.6e8}}}
+    r = bench.roofline(prof, n, k, launch)
+    t_store = 4.5e6 * 5e-12 + 3.5e6 * 16e-12
+    assert r["bound"] == "l2-store" and abs(r["frac"] - t_store / launch) < 1e-12
+    assert abs(r["peak"] - n * k / t_store) < 1e-3 * r["peak"] and r["traffic"] == 3.6e8
+    assert abs(r["achieved"] - n * k / launch) < 1e-6 * r["achieved"]
+    other = bench.roofline(prof, 8192, k, launch)             # profiled at 65,536 envs only
+    assert other["frac"] is None and "store bound unknown" in other["note"]
