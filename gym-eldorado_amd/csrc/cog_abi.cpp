@@ -155,8 +155,8 @@ bool zc_same_on(int device, const void *p) {
     ok = hipHostGetDevicePointer(&d, const_cast<uint8_t *>(base), 0) == hipSuccess && d == expect;
   }
   std::lock_guard<std::mutex> lk(g_zc_mu);
-  for (ZcRange &r : g_zc)
-    if (r.base == base) (ok ? r.same : r.differs) |= bit;
+  for (ZcRange &r : g_zc)   // (the same allocation: a view freed and re-allocated at `base` meanwhile
+    if (r.base == base && r.dev == expect) (ok ? r.same : r.differs) |= bit;   // may map elsewhere)
   return ok;
 }
 
@@ -206,19 +206,32 @@ int signal_enqueue(Signal &g, hipStream_t st) {
   g.queued = true;
   return COG_OK;
 }
+// the word, read with acquire semantics: the caller's later plain reads of the pinned views and
+// status words are not hoisted above it (x86 orders the loads; this orders the compiler)
+bool signal_seen(const Signal &g) {
+  return __atomic_load_n(const_cast<const uint32_t *>(g.h), __ATOMIC_ACQUIRE) == g.seq;
+}
 int signal_wait(Signal &g, hipStream_t st) {
+  const bool was_queued = g.queued;
   if (g.queued) {
     g.queued = false;
-    if (*g.h == g.seq) return COG_OK;
+    if (signal_seen(g)) return COG_OK;
     const auto t0 = std::chrono::steady_clock::now();
     const auto budget = std::chrono::microseconds(spin_budget_us());
     for (unsigned it = 1;; it++) {
-      if (*g.h == g.seq) return COG_OK;
+      if (signal_seen(g)) return COG_OK;
       __builtin_ia32_pause();
       if (!(it & 255u) && std::chrono::steady_clock::now() - t0 > budget) break;
     }
   }
   HIPCHK(hipStreamSynchronize(st));
+  // A kernel that stopped before all its workgroups arrived leaves the in-kernel counter non-zero,
+  // and the next armed kernel would store its word early: re-arm the counter whenever a queued
+  // word did not land by the time the stream drained.
+  if (was_queued && g.ctr && !signal_seen(g)) {
+    HIPCHK(hipMemsetAsync(g.ctr, 0, sizeof(uint32_t), st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
   return COG_OK;
 }
 

@@ -2506,8 +2506,11 @@ DEV void grid_signal(const GridSignal &g) {
   __syncthreads();
   if (threadIdx.x == 0) {
     __threadfence();                                       // this workgroup's stores performed
-    if (atomicAdd(g.ctr, 1u) == gridDim.x - 1) {
+    // acq_rel arrival + acquire fence in the last workgroup (as k_env_step_pub): every other
+    // workgroup's stores happen-before the release store of the word
+    if (__hip_atomic_fetch_add(g.ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
       __hip_atomic_store(g.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       __hip_atomic_store(g.word, g.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }

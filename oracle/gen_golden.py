@@ -146,9 +146,70 @@ def sampler_kat():
     return masks, acts
 
 
+# Whole workloads pinned by the reference: final-state digests of every env the reference can run
+# (name, n_envs, n_players, n_pieces, difficulty, seed, steps).  c5: bench.py's timed workload
+# (65,536 envs, seeds 12345 + i, sampler seeds the same; 5 warm-up + 1,200 steps, the length
+# tests/test_gpu_timed_workloads.py drives); c3: BASELINE config C3 at its own size.
+WORKLOADS = [("c5", 65536, 4, 3, 2, 12345, 1205), ("c3", 8192, 4, 3, 1, 12345, 1000)]
+
+
+def _ref_final_digests(job):
+    """Worker: the reference's own loop (ref_run_selected) for each listed env, digest at the end."""
+    seed0, idx, np_, npc, diff, steps = job
+    out = np.zeros((len(idx), 8), dtype=np.uint8)
+    for k, i in enumerate(idx):
+        r, s = po.RefVec1(), po.RefSampler1(seed0 + int(i))
+        r.reset(seed0 + int(i), np_, npc, diff, 100000)
+        r.run_selected(s, steps)
+        out[k] = np.frombuffer(digest_env(r, s.actions), dtype=np.uint8)
+    return out
+
+
+def workloads():
+    """Per workload: the oracle runs the whole batch (threaded) to find the envs the reference can
+    run (hazard flags), the reference runs each of those from its seed, and both final states'
+    digests must agree env by env (any difference aborts)."""
+    from multiprocessing import Pool
+    arrays, meta = {}, []
+    for name, n, np_, npc, diff, seed, steps in WORKLOADS:
+        o, s = po.OracleVec(n), po.OracleSampler(n, seed)
+        o.reset_threaded(seed, np_, npc, diff, 100000)
+        po.run_threaded(o, s, steps, po.host_threads())
+        flags = o.flags()
+        safe = (flags & po.REF_UNSAFE) == 0
+        idx = np.nonzero(safe)[0].astype(np.uint32)
+        odig = po.batch_digest(o.observations[idx], o.selected_action_masks[idx], o.rewards[idx], o.dones[idx],
+                               o.agent_selection[idx], o.infos[idx], s.actions[idx])
+        del o, s
+        jobs = [(seed, part, np_, npc, diff, steps) for part in np.array_split(idx, 64)]
+        with Pool(max(1, (os.cpu_count() or 2) - 1)) as pool:
+            rdig = np.concatenate(pool.map(_ref_final_digests, jobs))
+        bad = np.nonzero((rdig != odig).any(1))[0]
+        if bad.size:
+            raise SystemExit(f"{name}: oracle != reference at env {int(idx[bad[0]])} after {steps} steps")
+        arrays[f"{name}_safe"] = np.packbits(safe)
+        arrays[f"{name}_digests"] = rdig
+        meta.append(dict(name=name, n_envs=n, n_players=np_, n_pieces=npc, difficulty=diff, seed=seed,
+                         sampler_seed=seed, steps=steps, mode="sel", ref_envs=int(idx.size),
+                         oracle_only_envs=int(n - idx.size)))
+        print(f"{name}: {idx.size} of {n} envs pinned by the reference after {steps} steps "
+              f"({n - idx.size} hazard envs: oracle only)")
+    np.savez(os.path.join(OUT, "ref_workloads.npz"), **arrays)
+    with open(os.path.join(OUT, "ref_workloads.json"), "w") as f:
+        json.dump(dict(source="oracle/_ref (unmodified reference core) via oracle/gen_golden.py --workloads",
+                       digest="sha256[:8] per env over named leaves of obs, sel, rewards, dones, agent_sel, "
+                              "infos, actions after `steps` x (sample(selected masks); step) from reset",
+                       arrays="<name>_safe: packbits of the envs the reference ran; <name>_digests: "
+                              "uint8[ref_envs, 8] in env order",
+                       workloads=meta), f, indent=0)
+
+
 def main():
     assert po.ref_available(), "build the reference first: make -C oracle ref"
     os.makedirs(OUT, exist_ok=True)
+    if "--workloads" in sys.argv:
+        workloads()
+        return
     t = traces()
     arrays = {}
     for st in t:

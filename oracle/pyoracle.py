@@ -68,6 +68,27 @@ def step_digest(obs, sel, rewards, dones, agent_sel, infos, actions, nbytes=8):
     return h.digest()[:nbytes]
 
 
+def batch_digest(obs, sel, rewards, dones, agent_sel, infos, actions, nbytes=8, chunk=2048):
+    """step_digest of every env of a batch at once: row i equals step_digest(obs[i:i+1], ...,
+    actions[i:i+1]) (the same leaf names and leaf bytes, in the same order, hashed as one stream).
+    Returns uint8[n, nbytes]."""
+    arrays = (obs, sel, rewards, dones, agent_sel, infos, actions)
+    n = obs.shape[0]
+    out = np.zeros((n, nbytes), dtype=np.uint8)
+    for lo in range(0, n, chunk):
+        hi = min(n, lo + chunk)
+        parts = []
+        for a in arrays:
+            for nm, x in leaves(a[lo:hi]):
+                name = np.frombuffer(nm.encode(), dtype=np.uint8)
+                parts.append(np.broadcast_to(name, (hi - lo, name.size)))
+                parts.append(np.ascontiguousarray(x).reshape(hi - lo, -1).view(np.uint8))
+        rows = np.concatenate(parts, axis=1)
+        for j in range(hi - lo):
+            out[lo + j] = np.frombuffer(hashlib.sha256(rows[j].tobytes()).digest()[:nbytes], dtype=np.uint8)
+    return out
+
+
 def named_equal(a, b):
     """Compare two structured arrays field by field; return the first differing leaf or None."""
     for (n, x), (_, y) in zip(leaves(a), leaves(b)):
@@ -142,6 +163,8 @@ class _Lib:
             lib.ref_layout_name.argtypes = [C.c_int]
             lib.ref_layout_offset.restype = C.c_size_t
             lib.ref_layout_offset.argtypes = [C.c_int]
+            lib.ref_run_selected.restype = C.c_int
+            lib.ref_run_selected.argtypes = [vp, vp, C.c_int]
             cls._ref = lib
         return cls._ref
 
@@ -273,6 +296,11 @@ class RefVec1:
     def step(self, actions):
         actions = np.ascontiguousarray(actions, dtype=ACTION)
         if self.lib.ref_step(self.h, actions.ctypes.data):
+            raise RuntimeError("Failed to generate map in specified maximum number of attempts")
+
+    def run_selected(self, sampler, steps):
+        """`steps` x (sampler.sample(selected_action_masks); step(actions)) inside the reference."""
+        if self.lib.ref_run_selected(self.h, sampler.h, int(steps)):
             raise RuntimeError("Failed to generate map in specified maximum number of attempts")
 
     def __del__(self):

@@ -117,6 +117,24 @@ void ref_sample(void *s, const void *mask) {
 const void *ref_sampler_actions(void *s) { return static_cast<smp1 *>(s)->get_actions().data(); }
 }
 
+// The reference's own loop for one env (benchmarks/benchmarks.py:47-51 with the runner's
+// mask source, include/runner.h:46-55): `steps` x (sample(selected_action_masks); step(actions)),
+// in C so that fixtures of whole timed workloads (tens of thousands of envs x ~1,000 steps) are
+// cheap to generate.  0, or -1 when a reset inside the loop failed.
+extern "C" int ref_run_selected(void *h, void *s, int steps) {
+  env1 *e = static_cast<env1 *>(h);
+  smp1 *q = static_cast<smp1 *>(s);
+  try {
+    for (int t = 0; t < steps; t++) {
+      q->sample(e->get_selected_action_masks());
+      e->step(q->get_actions());
+    }
+  } catch (const generate_map_failure &) {
+    return -1;
+  }
+  return 0;
+}
+
 // Calibration only: the reference's own sequential loop (vec_cog_env<1>::step + action_sampler)
 // over n envs with the given (hazard-free) seeds, `steps` x (sample(selected mask); step).
 #include <chrono>
