@@ -339,60 +339,71 @@ def cpu_baseline(seconds):
                       f"(best of thread counts {counts})"}
 
 
-def roofline(prof, n, k_chunk, launch_s):
-    """The dominant kernel k_env_rollout against what bounds it: its per-step output stores through
-    L2 (profiles/r03_store_bound.txt).  Every step stores the ~6.2 changed 16-B granules of each
-    env's records (ObsData tail, selected mask, Info byte, action); at 65,536 envs an XCD's share of
-    those lines exceeds its 4 MiB L2, so about half the stores miss and each costs a fabric
-    write-back.  Store bound of one launch: T_store = hits x c_hit + misses x c_miss, with the
-    launch's L2 write hits / misses from a rocprofv3 --pmc pass of this exact engine source and
-    c_hit / c_miss the measured cost of a scattered 16-B store that hits / misses L2 on this chip
-    (tools/storeprobe.hip, both in profiles/pmc_profile.json).  achieved = env-steps/s of the
-    launch timed here (HIP events); peak = env-steps/s if the launch took T_store; frac = T_store
-    / launch time.  Beside it: counter HBM traffic and the VALU issue rate (secondary bounds)."""
+KERNEL_LABEL = {"wave": "k_env_rollout<selected>", "pipe": "k_env_rollout_pipe<selected>",
+                "duo": "k_env_rollout_duo<selected> + k_env_fixup<selected>",
+                "trio": "k_env_rollout_trio<selected> + k_env_fixup<selected>"}
+
+
+def roofline(prof, n, k_chunk, launch_s, kind="wave"):
+    """The dominant kernel -- the persistent rollout that runs a shard of n envs (`kind`: wave,
+    pipe, duo or trio, cog_rollout_kind) -- against what bounds it: its per-step output stores through L2
+    (profiles/r03_store_bound.txt).  Every step stores the ~6.2 changed 16-B granules of each env's
+    records (ObsData tail, selected mask, Info byte, action); at 65,536 envs an XCD's share of those
+    lines exceeds its 4 MiB L2, so about half the stores miss and each costs a fabric write-back.
+    Store bound of one launch: T_store = hits x c_hit + misses x c_miss, with the launch's L2 write
+    hits / misses from a rocprofv3 --pmc pass of this exact engine source AT THIS LAUNCH SHAPE (n
+    envs, k steps per launch: profiles/pmc_profile.json `rollouts`) and c_hit / c_miss the measured
+    cost of a scattered 16-B store that hits / misses L2 on this chip (tools/storeprobe.hip).
+    achieved = env-steps/s of the launch timed here (HIP events); peak = env-steps/s if the launch
+    took T_store; frac = T_store / launch time.  Beside it: the counter HBM traffic of the same
+    shape and the VALU issue rate.  No profile of this shape: traffic, peak and frac are null."""
     waves = (n + 63) // 64
     valu_peak = N_SIMD * CLOCK_HZ / VALU_CYC                # wave64 VALU instructions per second
-    out = {"bound": "l2-store", "kernel": "k_env_rollout<selected>", "unit": "env-steps/s",
+    out = {"bound": "l2-store", "kernel": KERNEL_LABEL.get(kind, kind), "rollout_kind": kind, "unit": "env-steps/s",
            "achieved": n * k_chunk / launch_s, "peak": None, "frac": None, "traffic": None,
            "kernel_ms": launch_s * 1e3, "steps_per_launch": k_chunk, "envs_per_launch": n}
     alg = STEP_BYTES * n * k_chunk
     out["hbm"] = {"survey_8d_bytes_per_launch": alg, "survey_8d_GBs": alg / launch_s / 1e9,
                   "note": "800 B/env-step (SURVEY 8d) assumes every step reads its state from HBM; "
                           "the rollout keeps it on-chip, so this rate can exceed the HBM peak"}
-    r = (prof or {}).get("k_env_rollout")
-    key = str(k_chunk)
-    l2 = ((r or {}).get("l2_per_launch") or {}).get(key)
+    e = ((prof or {}).get("rollouts") or {}).get("%d:%d" % (n, k_chunk))
+    if e and e.get("kind") != kind:
+        e = None                                          # profiled with another rollout kernel
     sc = (prof or {}).get("store_costs")
-    if l2 and sc and r.get("envs_per_launch") == n:
+    l2 = (e or {}).get("l2_per_launch")
+    if l2 and sc:
         t_store = l2["hits"] * sc["c_hit_s"] + l2["misses"] * sc["c_miss_s"]
         out.update(peak=n * k_chunk / t_store, frac=t_store / launch_s,
                    store_model={"l2_write_requests_per_env_step": l2["writes"] / n / k_chunk,
                                 "l2_hits_per_launch": l2["hits"], "l2_misses_per_launch": l2["misses"],
+                                "l2_hit_rate": l2["hits"] / max(1.0, l2["hits"] + l2["misses"]),
                                 "fabric_write_requests_per_launch": l2.get("fabric_write_requests"),
                                 "c_hit_s": sc["c_hit_s"], "c_miss_s": sc["c_miss_s"],
                                 "t_store_s": t_store, "t_kernel_s": launch_s})
+        if kind != "wave":
+            out["note"] = ("shards of <= 32,768 envs keep their written lines in L2: the store bound is "
+                           "far from the launch time, which the stepping wave's instruction latency sets "
+                           "(DESIGN.md 7)")
     else:
-        out["note"] = "no PMC profile of this engine source at %d envs x %d steps (tools/pmc_profile.py): " \
-                      "store bound unknown" % (n, k_chunk)
-    if r and r.get("valu_per_wave_step"):
-        per_ws = r["valu_per_wave_step"]
-        achieved = per_ws * waves * k_chunk / launch_s
+        out["note"] = "no PMC profile of this engine source at %d envs x %d steps (%s; tools/pmc_profile.py): " \
+                      "store bound unknown" % (n, k_chunk, kind)
+    if e and e.get("bytes_per_launch") is not None:
+        tr = e["bytes_per_launch"] + ((e.get("companion") or {}).get("bytes_per_launch") or 0.0)
+        out["traffic"] = tr
+        out["hbm"]["counter_GBs"] = tr / launch_s / 1e9
+        out["hbm"]["counter_frac"] = tr / launch_s / 1e9 / HBM_PEAK_GBS
+        out["hbm"]["counter_bytes_per_env_step"] = tr / n / k_chunk
+    pw = (e or {}).get("per_wave_step") or {}
+    if pw.get("valu"):
+        achieved = pw["valu"] * waves * k_chunk / launch_s
         out["valu_issue"] = {
             "achieved": achieved, "peak": valu_peak, "frac": achieved / valu_peak, "unit": "VALU wave-instr/s",
-            "valu_per_wave_step": per_ws, "salu_per_wave_step": r.get("salu_per_wave_step"),
-            "issue_quads_per_wave_step": r.get("active_inst_any_per_wave_step"),
-            "wait_quads_per_wave_step": r.get("wait_any_per_wave_step"),
-            "wave_quads_per_wave_step": r.get("wave_cycles_per_wave_step"),
-            "note": "peak = 1,024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU; not the bound: a lone wave "
-                    "of this kernel uses about a quarter of its SIMD's VALU rate (profiled at %d envs x %d "
-                    "steps per launch)" % (r.get("envs_per_launch", 0), r.get("steps_per_launch", 0))}
-        tr = r.get("bytes_per_step_launch", {})
-        if key in tr:
-            out["traffic"] = tr[key]
-            out["hbm"]["counter_GBs"] = tr[key] / launch_s / 1e9
-            out["hbm"]["counter_frac"] = tr[key] / launch_s / 1e9 / HBM_PEAK_GBS
-        elif "per_env_step" in r:
-            out["hbm"]["counter_bytes_per_env_step"] = r["per_env_step"]
+            "valu_per_wave_step": pw["valu"], "salu_per_wave_step": pw.get("salu"),
+            "issue_quads_per_wave_step": pw.get("active_inst_any"), "wait_quads_per_wave_step": pw.get("wait_any"),
+            "wave_quads_per_wave_step": pw.get("wave_cycles"),
+            "note": "peak = 1,024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU; per 64-env wave and step (the duo / trio / "
+                    "pipe: every wave of the workgroup); not the bound at 65,536 envs, where a lone wave of this "
+                    "kernel uses about a quarter of its SIMD's VALU rate"}
     return out
 
 
@@ -448,7 +459,7 @@ def main():
     k_chunk = min(chunk, args.steps)
     launch_s = kernel_time(runner, k_chunk, max(3, min(20, 4000 // max(k_chunk, 1))))
     prof = load_profile()
-    roof = roofline(prof, n, k_chunk, launch_s)
+    roof = roofline(prof, n, k_chunk, launch_s, cg._city_of_gold.rollout_kind(n, N_PLAYERS, False))
 
     haz, per = env.hazards()
     n_erase = int(((per & HAZ_ERASE_PAST) != 0).sum())
@@ -462,8 +473,9 @@ def main():
                                  us_per_step(cg, n, dev),
                                  "us_per_step_at_%d" % N_SHARD8: us_per_step(cg, N_SHARD8, dev),
                                  "note": "rollout device time per step, 1,000-step launches; shards of <= 32,768 "
-                                         "envs (the N=8 shard: 8,192 = 128 workgroups) take the two-wave "
-                                         "rollout, a second wave per workgroup issuing the store phase"}
+                                         "envs (the N=8 shard: 8,192 = 128 workgroups) take the trio rollout: "
+                                         "a stepping wave, a wave for the deferred turn ends' draws and a wave "
+                                         "issuing the store phase per workgroup"}
         # one kernel launch per step (the runner's step() path)
         pl_steps = 500
         runner.set_chunk(1)

@@ -284,6 +284,7 @@ struct EnvShard {
 
 struct cog_env {
   size_t n = 0;
+  uint8_t n_players = 4;              // the batch's players (reset params; the default ctor's 4)
   std::vector<EnvShard> sh;
   uint32_t *h_err = nullptr;          // pinned, device-mapped: one error word per shard (256 B apart)
   // host views: obs is one pinned allocation; the small records are the shard's h_outs block
@@ -623,6 +624,9 @@ extern "C" {
 
 const char *cog_last_error(void) { return g_err.c_str(); }
 int cog_abi_version(void) { return COG_ABI_VERSION; }
+int cog_rollout_kind(size_t n_envs, int n_players, int stored_masks) {
+  return cog::rollout_kind_of(n_envs, stored_masks ? cog::MASK_STORED : cog::MASK_SELECTED, n_players >= 3);
+}
 
 int cog_device_count(int *out) {
   if (!out) return fail(COG_ERR_INVALID, "out is NULL");
@@ -695,6 +699,7 @@ int cog_env_shard_info(const cog_env *env, int k, size_t *first, size_t *count, 
 static int env_reset_impl(cog_env *e, const cog::ResetParams &p) {
   int rc = prepare_host(e);
   if (rc) return rc;
+  if (p.use_params) e->n_players = p.n_players;
   for (EnvShard &k : e->sh) {
     k.done.queued = false;
     k.host_synced = false;                                 // (refresh_full: the mirror is rebuilt later)
@@ -957,8 +962,13 @@ static int time_copy_variants(int device, size_t bytes, int iters, double *gb_pe
               hipEventCreate(&e1) != hipSuccess || hipMemsetAsync(a, 1, bytes, st) != hipSuccess))
     rc = fail(COG_ERR_HIP, "copy setup");
   double best = 0.0;
-  const int v0 = mix ? 8 : 0, v1 = mix ? 10 : 8;         // the fastest variant
-  for (int v = v0; v < v1 && !rc; v++) {
+  // the fastest variant: copy 0-7 (grid stride / one pass, plain / non-temporal) and 16-17 (one
+  // granule per work-item); the mix 8-9
+  static const int kCopyVariants[] = {0, 1, 2, 3, 4, 5, 6, 7, 16, 17}, kMixVariants[] = {8, 9};
+  const int *vs = mix ? kMixVariants : kCopyVariants;
+  const int nv = mix ? 2 : 10;
+  for (int j = 0; j < nv && !rc; j++) {
+    const int v = vs[j];
     if (cog::launch_copy_peak(a, b, bytes, st, v)) rc = fail(COG_ERR_HIP, "copy launch failed");   // warm-up
     if (rc) break;
     (void)hipEventRecord(e0, st);
@@ -1252,7 +1262,8 @@ static int runner_launch_fused(cog_runner *r, int steps) {
     const cog::DevState s = launch_state(k, host);
     if (r->chunk > 1) {                                    // persistent kernels, chunk steps each
       for (int t = 0; t < steps; t += r->chunk)
-        if (cog::launch_rollout(s, src, std::min(r->chunk, steps - t), q.d_rng, q.d_actions, k.stream))
+        if (cog::launch_rollout(s, src, std::min(r->chunk, steps - t), q.d_rng, q.d_actions, k.stream,
+                                r->env->n_players >= 3))
           return fail(COG_ERR_HIP, std::string("rollout launch failed: ") + hipGetErrorString(hipGetLastError()));
     } else {
       for (int t = 0; t < steps; t++)

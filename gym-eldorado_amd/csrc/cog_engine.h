@@ -108,6 +108,10 @@ struct DevState {
   // direct publish (launch_step_pub only; null otherwise): device addresses of the shard's pinned
   // ObsData view and outs block, and the publish mirror (k_publish's `mir`)
   uint8_t *pub_obs, *pub_outs, *pub_mir;
+  // test hook ($COG_DEBUG_REDO_STEP, launch_rollout): the duo rollout's deferred turn end parks
+  // every env at this step of each launch as if its action drew from the env rng (kParkRedo), so
+  // the tests exercise that path; -1 (default): off
+  int32_t redo_at;
 };
 
 struct ResetParams {
@@ -153,13 +157,17 @@ size_t publish_mirror_bytes(size_t n, size_t outs_bytes);
 bool publish_can_signal(size_t n, size_t outs_bytes, bool actions);
 int launch_sample_step(const DevState &s, int mask_source, uint32_t *d_rng, uint8_t *d_actions,
                        void *stream);
+// persistent K-step runner loop; defer_ok: every env of the shard has >= 3 players (the trio
+// rollout's deferred turn end may run on shards of <= 16,384 envs with the selected masks)
 int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions,
-                   void *stream);                    // persistent K-step runner loop
+                   void *stream, bool defer_ok = false);
+int rollout_kind_of(size_t n, int mask_source, bool defer_ok);   // 0 duo, 1 wave, 2 pipe, 3 trio (launch_rollout)
 int launch_seed_sampler(size_t n, uint64_t seed, size_t first, uint32_t *d_rng, void *stream);
 // completion word: stores seq into *d_word (device address of a pinned host word) once every
 // earlier packet of the stream has completed
 int launch_signal(uint32_t *d_word, uint32_t seq, void *stream);
-// variant bit 0: non-temporal loads/stores; bit 1: 32 waves per CU instead of 8 (grid stride);
+// variant bit 0: non-temporal loads/stores; bit 4: one granule per work-item (bits 1-3 ignored);
+// bit 1: 32 waves per CU instead of 8 (grid stride);
 // bit 2: one pass, 32 KiB per workgroup (bit 1 ignored); bit 3: the encode's 1:7 read:write mix
 // (reads `bytes`, writes 7 x `bytes` into dst; bit 0 = non-temporal stores); bytes: a multiple of 16
 int launch_copy_peak(const void *src, void *dst, size_t bytes, void *stream, int variant);

@@ -1873,6 +1873,18 @@ struct RegEnv {
                             (coins > 5.f ? kCostMask5 : 0u);
     return 1u | ((avail & afford) << 1);
   }
+  // Player::end_turn's deck part (player.cpp:170-180, cards.cpp:219-232,183-211): discard the
+  // active and played piles, draw up to the hand size.  NQ by the wave's `wide` ballot (see draw).
+  DEV void end_turn_deck() {
+    const int n_draw = COG_HAND_SIZE - (int)P.n_in_hand;
+    if (__builtin_amdgcn_ballot_w64(P.pad != 0u)) {        // a deck of the wave holds a type >= 8
+      discard_all<6>();
+      if (n_draw > 0) draw<6>((uint32_t)n_draw);
+    } else {
+      discard_all<2>();
+      if (n_draw > 0) draw<2>((uint32_t)n_draw);
+    }
+  }
   // special actions (cards.cpp:8-36, the remove lambda environment.cpp:156-158) on the stored
   // mask `m` of the current agent and the selected mask, for the acting player (:183-186)
   DEV void apply_special(int special, Heads &m) {
@@ -1994,6 +2006,10 @@ DEV void dup_sink(const RegEnv &R2) {
 }
 #endif
 
+// DEFER (the trio rollout's deferred turn end): the turn end's discard and draws are left to the
+// drawing wave (trio_drawer), which owns the env rng -- the acting player's counters (n_active =
+// 0) and the saved mask (the selected mask before the draws) go out as they stand.
+template <bool DEFER = false>
 DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i, int na PH_PARAM) {
   const int ag = (int)R.agent();
   PState &P = R.P;
@@ -2157,15 +2173,8 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
     }
 #endif
     P.n_active = 0;                                        // Player::end_turn (player.cpp:170-180)
-    const int n_draw = COG_HAND_SIZE - (int)P.n_in_hand;
     PH(9);
-    if (__builtin_amdgcn_ballot_w64(P.pad != 0u)) {        // a deck of the wave holds a type >= 8
-      R.discard_all<6>();
-      if (n_draw > 0) R.draw<6>((uint32_t)n_draw);
-    } else {
-      R.discard_all<2>();
-      if (n_draw > 0) R.draw<2>((uint32_t)n_draw);
-    }
+    if (!DEFER) R.end_turn_deck();
     PH(10);
     R.sta = R.sel;                                         // save_actionmask
     R.set_agent((uint32_t)na);
@@ -2699,7 +2708,11 @@ DEV void lds_players(const LaneLds &L, int l, int ag, int na, Snap &S) {
 // the outputs are those of one full-step loop; the lean loop keeps the reset path's registers
 // out of its allocation.  A wave with nothing parked ends after the lean pass (round 1 launched
 // the fix-up as a second kernel: 4.8 us per launch even when it had nothing to do).
-constexpr uint32_t kParkNone = ~0u, kParkFinish = 1u << 31;
+// park codes: bits 0..29 the step t; kParkFinish: step t finished the episode (else the env
+// started step t done); kParkRedo: step t was not run (the duo rollout's deferred turn end met an
+// action that draws from the env rng, duo_stepper) -- the fix-up runs it with the full step
+constexpr uint32_t kParkNone = ~0u, kParkFinish = 1u << 31, kParkRedo = 1u << 30;
+constexpr uint32_t kParkStep = kParkRedo - 1u;
 // The records of a wave's envs seen from the wave's first env: a per-wave (scalar) base and a
 // per-lane index below 64, so that record addresses are a scalar base plus a 32-bit lane offset
 // (the saddr form of global loads and stores) instead of 64-bit products of a global index,
@@ -2845,8 +2858,10 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s_glob, int steps, uin
   if (FIX) {                                               // step `park`'s episode end
     bool enc = false, rs = false;
     uint32_t agent = 0;
-    if (live) {
-      t_first = (int)(park & ~kParkFinish) + 1;
+    if (live && (park & kParkRedo)) {                      // step `park` itself was not run
+      t_first = (int)(park & kParkStep);
+    } else if (live) {
+      t_first = (int)(park & kParkStep) + 1;
       agent = S.g1.y & 0xffu;
       const bool finish = (park & kParkFinish) != 0u;
       rs = end_of_step_a(s, i, !finish, finish, agent, out);
@@ -2869,7 +2884,7 @@ DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s_glob, int steps, uin
   __builtin_amdgcn_s_waitcnt(0);
   if (PIPE && !FIX) __syncthreads();                       // the decks in LDS: the storing wave's image
   PH_DECL;
-  for (int t = FIX ? 1 : 0; t < steps; t++) {
+  for (int t = 0; t < steps; t++) {
     if (PIPE) {                                            // every lane, every step: the records
       if (t) __syncthreads();                              // of step t - 1 to the storing wave
       if (!live) O->g[t & 1][13][l] = make_uint4(0u, 0u, 0u, 0u);   // (no record)
@@ -3093,19 +3108,47 @@ constexpr uint32_t kMetaValid = 1u, kMetaMoved = 2u, kMetaEnded = 1u << 16;
 
 DEV uint32_t next_player(uint32_t a, uint32_t np) { return a + 1u >= np ? 0u : a + 1u; }
 
-// every private record of env i from the stepping wave (registers + the wave's LDS)
-DEV void duo_store_private_all(const DevState &s, size_t i, const RegEnv &R, const DuoLds &D, int l) {
+// The env-level private records of env i from the stepping wave's registers (EnvPriv granules
+// 0, 1, 3, the selected mask's bits).  The player records (counters, neighbourhood caches,
+// stored-mask bits) are stored from the wave's LDS by the epilogue (lds_store_wave), parked envs'
+// included, after the last update of them.  DEFER (the trio): the env rng is the drawing wave's
+// (it stores it at its end), so granule 0's first dword is left alone.
+template <bool DEFER>
+DEV void duo_store_env_private(const DevState &s, size_t i, const RegEnv &R) {
   uint4 *pw = reinterpret_cast<uint4 *>(s.priv + i);
-  pw[0] = make_uint4(R.rng, R.seed, R.max_steps, R.turn_counter);
+  if (DEFER) reinterpret_cast<uint3 *>(reinterpret_cast<uint32_t *>(pw) + 1)[0] = make_uint3(R.seed, R.max_steps, R.turn_counter);
+  else pw[0] = make_uint4(R.rng, R.seed, R.max_steps, R.turn_counter);
   pw[1] = make_uint4(R.g1x, R.g1y, R.in_market, R.flags);
   reinterpret_cast<uint32_t *>(pw + 3)[0] = R.info_steps;
   s.heads[5 * i] = mbits_u4(bits_of(R.sel));
-#pragma unroll
-  for (int p = 0; p < 4; p++) {
-    pw[4 + p] = D.pl[p][l];
-    reinterpret_cast<uint2 *>(pw + 8)[p] = D.cells[p][l];
-    s.heads[5 * i + 1 + p] = D.heads[p][l];
+}
+
+// The deferred turn end (the trio rollout: selected masks, >= 3 players).  The stepping wave ends
+// a turn without touching the deck -- no discard, no draws -- and the drawing wave completes it
+// from the step record (the acting player's deck after the step, its counters in `pl`, the saved
+// mask) with the env rng, which it owns: Player::end_turn's discard + draw (player.cpp:170-180),
+// then the saved mask gains the drawn cards (draw's mask updates, cards.cpp:183-211, precede
+// save_actionmask).  Nothing the stepping wave reads before that player acts again depends on it:
+// with >= 3 players the next two agents are other players, whose turn ends lie at least two steps
+// back.  An action that would draw from the env rng inside a step (step_draws_rng: never taken in
+// the canonical loop) parks the env with kParkRedo, and k_env_fixup runs that step and
+// the rest with the full step.
+// DEFER: whether step_regs would draw from the env rng for this action -- a special that draws
+// cards (cards.cpp:8-36) or a move whose requirement discards / removes random active cards
+// (player.cpp:85-131) -- the same dispatch as step_regs (environment.cpp:104-160)
+DEV bool step_draws_rng(const RegEnv &R, const uint8_t act[5]) {
+  if (act[0]) return false;                                // play_card
+  if (act[1]) {
+    const uint32_t sp = cardf(kSpecial, act[1] - 1);
+    return sp == COG_SPECIAL_DRAW2 || sp == COG_SPECIAL_DRAW3 || sp == COG_SPECIAL_DRAW1_REMOVE1 ||
+           sp == COG_SPECIAL_DRAW2_REMOVE2;
   }
+  if (act[3] && !R.P.next_move_free) {
+    const uint64_t v = (uint64_t)R.cells_a.x | (uint64_t)R.cells_a.y << 32;
+    const uint32_t req = COG_HEX_REQ((uint32_t)(v >> (8 * act[3])) & 0xffu);
+    return req == COG_REQ_REMOVE || req == COG_REQ_DISCARD;
+  }
+  return false;
 }
 
 template <int SRC>
@@ -3203,7 +3246,7 @@ DEV void duo_stepper(DuoLds &D, const DevState &s_glob, int steps, uint32_t *__r
         R.na_active = (D.pl[na1][l].y >> 16) & 0xffu;
       }
       if (ended) {                                         // hand the env to k_env_fixup
-        duo_store_private_all(s, i, R, D, l);
+        duo_store_env_private<false>(s, i, R);
         rngs[i] = srng;
         park = (uint32_t)t | (finish ? kParkFinish : 0u);
         live = false;
@@ -3220,11 +3263,7 @@ DEV void duo_stepper(DuoLds &D, const DevState &s_glob, int steps, uint32_t *__r
   __syncthreads();                                         // X_steps
   PH_FLUSH(s_glob);
   if (live) {                                              // env-level private state back to HBM
-    uint4 *pw = reinterpret_cast<uint4 *>(s.priv + i);
-    pw[0] = make_uint4(R.rng, R.seed, R.max_steps, R.turn_counter);
-    pw[1] = make_uint4(R.g1x, R.g1y, R.in_market, R.flags);
-    reinterpret_cast<uint32_t *>(pw + 3)[0] = R.info_steps;
-    s.heads[5 * i] = mbits_u4(bits_of(R.sel));
+    duo_store_env_private<false>(s, i, R);
     rngs[i] = srng;
   }
   if (l < ne) s.park[i] = park;
@@ -3254,6 +3293,32 @@ DEV void setm(MBits b[4], int p, const MBits &v) {
     b[q].w1 = p == q ? v.w1 : b[q].w1;
     b[q].w2 = p == q ? v.w2 : b[q].w2;
   }
+}
+
+// DEFER: the turn end of record t's acting player ag (meta: ag1 != ag), on the drawing wave --
+// Player::end_turn's discard + draw on the deck as the step left it, with the env rng; the saved
+// mask gains the drawn cards; the player's counters and stored-mask bits go back to the LDS
+// records the stepping wave reads when ag acts again.
+template <class Lds>
+DEV void duo_turn_end(Lds &D, int l, int ag, uint4 dk[7], MBits &ba, uint32_t &rng) {
+  RegEnv E;
+#pragma unroll
+  for (int k = 0; k < 7; k++) {
+    E.d[4 * k] = dk[k].x; E.d[4 * k + 1] = dk[k].y; E.d[4 * k + 2] = dk[k].z; E.d[4 * k + 3] = dk[k].w;
+  }
+  E.P = unpack_player(D.pl[ag][l]);
+  E.rng = rng;
+  E.sel = heads_of(ba);
+  E.flags = 0u;
+  E.tab = D.tab;
+  E.end_turn_deck();
+#pragma unroll
+  for (int k = 0; k < 7; k++) dk[k] = make_uint4(E.d[4 * k], E.d[4 * k + 1], E.d[4 * k + 2], E.d[4 * k + 3]);
+  ba = bits_of(E.sel);
+  rng = E.rng;
+  D.pl[ag][l] = pack_player(E.P);
+  D.heads[ag][l] = mbits_u4(ba);
+  if (E.flags) D.sflags[l] |= E.flags;
 }
 
 DEV void duo_storer(DuoLds &D, const DevState &s_glob, int steps, uint8_t *__restrict__ actions_glob) {
@@ -3359,10 +3424,325 @@ __global__ void __launch_bounds__(128) k_env_rollout_duo(DevState s, int steps, 
   if (role == 0) {
 #ifndef DUO_NOPRIO                                         // (diagnostic A/B builds only)
     __builtin_amdgcn_s_setprio(3);                         // the stepping wave wins VALU issue on
-#endif
-    duo_stepper<SRC>(D, s, steps, rngs);                   // a SIMD it shares with a storing wave
+#endif                                                     // a SIMD it shares with a storing wave
+    duo_stepper<SRC>(D, s, steps, rngs);
   } else {
     duo_storer(D, s, steps, actions_out);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Trio rollout (round 4): the duo with the turn end's discard + draws deferred to a wave of their
+// own, for the selected-mask loop with >= 3 players on shards of <= 16,384 envs.  Tried first with
+// the duo's two waves, the storing wave doing the draws (profiles/r04d_duo_defer.txt, 8,192
+// envs): deferring cut the stepping wave's work from 6,340 to 5,040 ticks per step, but the
+// storing wave then carried its stores (2,790) and the draws (2,100) and set the pace at 7,900 --
+// so the draws go to a third wave, and the storing wave's deck image moves to LDS (the stepping
+// wave takes the next agent's deck straight from it: no per-step hand-over copy).
+//
+// Per step t the stepping wave writes record t (ring[t & 1], deckr[t % 3]); the drawing wave
+// completes record t's turn ends in [Y_t, X_{t+1}] (the env rng is its own: it rewrites the
+// record's deck and saved mask in place, and the player's counters and stored-mask bits in
+// pl / heads); the storing wave stores record t one step later, in [Y_{t+1}, X_{t+2}], and updates
+// the deck image.  The loop runs steps + 1 rounds (the last drains the pipeline), then one more
+// barrier; every wave executes every barrier.  Why the reads are safe: the stepping wave reads a
+// player's deck image, counters or stored mask only when that player is the next agent or the one
+// after it, and with >= 3 players every turn end of that player lies at least two steps back --
+// its record is through both waves by then (the deferred turn end note above step_draws_rng).
+struct TrioLds {
+  uint4 img[4][7][64];                // every player's DeckObs as last stored (the storing wave's image)
+  uint4 deckr[3][7][64];              // record t's DeckObs (acting player after the step), t % 3
+  uint4 ring[2][kRingG][64];          // record t (duo layout), t & 1
+  uint4 pl[4][64];
+  uint2 cells[4][64];
+  uint4 heads[4][64];
+  uint32_t sflags[64];                // hazard flags of the drawing wave's draws
+  UidEntry tab[kUidTab];
+};
+
+template <int SRC>
+DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, uint32_t *__restrict__ rngs_glob) {
+  const int l = threadIdx.x;
+  const size_t wbase = (size_t)blockIdx.x * 64;
+  const DevState s = wave_view(s_glob, wbase);
+  const size_t i = (size_t)l;
+  const int ne = (int)min((size_t)64, s_glob.n - wbase);
+  uint32_t *__restrict__ rngs = rngs_glob + wbase;
+  bool live = l < ne;
+  uint32_t park = kParkNone, srng = 0;
+  RegEnv R;
+  int ag = 0, na = 0;
+  if (live) {
+    Snap S;
+    load_env(s, i, S);
+    regs_env(R, S);
+    const uint4 *pv4 = reinterpret_cast<const uint4 *>(s.priv + i);
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+      D.pl[p][l] = pv4[4 + p];
+      D.cells[p][l] = reinterpret_cast<const uint2 *>(pv4 + 8)[p];
+      D.heads[p][l] = s.heads[5 * i + 1 + p];
+    }
+    srng = rngs[i];
+    ag = (int)R.agent();
+    na = (int)next_player((uint32_t)ag, R.n_players());
+    R.P = unpack_player(D.pl[ag][l]);
+    R.na_active = (D.pl[na][l].y >> 16) & 0xffu;
+    R.cells_a = D.cells[ag][l];
+    R.cells_n = D.cells[na][l];
+    R.sta = heads_of(mbits_of(D.heads[ag][l]));
+    R.stn = heads_of(mbits_of(D.heads[na][l]));
+  }
+  R.tab = D.tab;
+  __builtin_amdgcn_s_waitcnt(0);                           // (no per-iteration vmcnt wait covers them)
+  __syncthreads();                                         // B: the storing wave loaded every deck
+  if (live) {
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+      const uint4 v = D.img[ag][k][l];
+      R.d[4 * k] = v.x; R.d[4 * k + 1] = v.y; R.d[4 * k + 2] = v.z; R.d[4 * k + 3] = v.w;
+    }
+  }
+  PH_DECL;
+  int b3 = 0;                                              // t % 3
+  for (int t = 0; t <= steps; t++) {
+    bool ended = false, finish = false;
+    uint8_t act[5];
+    if (t < steps && live) {
+      const uint32_t srng0 = srng;
+      step_action<SRC>(R, make_uint2(0u, 0u), srng, act);
+      bool redo = false;
+      const bool rare = !act[0] && (act[1] | act[3]) != 0;
+      if (__builtin_amdgcn_ballot_w64(rare) && rare) redo = step_draws_rng(R, act);
+      redo = redo || t == s.redo_at;                       // (test hook, -1: off)
+      if (redo) {                                          // hand the env to k_env_fixup, step t not run
+        srng = srng0;
+        duo_store_env_private<true>(s, i, R);
+        rngs[i] = srng;
+        park = (uint32_t)t | kParkRedo;
+        live = false;
+      } else {
+        const bool was_done = R.done() != 0u;
+        finish = !was_done && step_regs<true>(R, act, s, i, na PH_PASS);
+        if (finish) R.set_done(1u);
+        ended = was_done || finish;
+        PH(0);
+        D.pl[ag][l] = pack_player(R.P);
+        D.cells[ag][l] = R.cells_a;
+        D.heads[ag][l] = mbits_u4(bits_of(R.sta));
+        if (na != ag) D.heads[na][l] = mbits_u4(bits_of(R.stn));
+#pragma unroll
+        for (int k = 0; k < 7; k++)
+          D.deckr[b3][k][l] = make_uint4(R.d[4 * k], R.d[4 * k + 1], R.d[4 * k + 2], R.d[4 * k + 3]);
+        PH(1);
+      }
+    }
+    __syncthreads();                                       // X_t
+    PH(2);
+    if (t < steps) {
+      if (live) {
+        const int ag1 = (int)R.agent();
+        const int na1 = (int)next_player((uint32_t)ag1, R.n_players());
+        const MBits bs = bits_of(R.sel), ba = bits_of(R.sta), bn = bits_of(R.stn);
+        const uint32_t info = (R.info_steps >> (8 * ag)) & 0xffu;
+        const uint32_t meta = kMetaValid | (R.moved ? kMetaMoved : 0u) | (uint32_t)ag << 2 | (uint32_t)na << 4 |
+                              (uint32_t)na1 << 6 | info << 8 | (ended ? kMetaEnded : 0u) | (uint32_t)ag1 << 24;
+        uint4(*ring)[64] = D.ring[t & 1];
+#pragma unroll
+        for (int k = 0; k < 3; k++) ring[k][l] = make_uint4(R.sh[4 * k], R.sh[4 * k + 1], R.sh[4 * k + 2], R.sh[4 * k + 3]);
+        ring[3][l] = make_uint4(bs.w0, bs.w1, bs.w2, meta);
+        ring[4][l] = make_uint4(ba.w0, ba.w1, ba.w2,
+                                (uint32_t)act[0] | (uint32_t)act[1] << 8 | (uint32_t)act[2] << 16 | (uint32_t)act[3] << 24);
+        ring[5][l] = make_uint4(bn.w0, bn.w1, bn.w2, (uint32_t)act[4]);
+        ring[6][l] = R.g2;
+        R.moved = false;
+        if (ag1 != ag) {                                   // turn change: ag1 == na acts next, its deck
+#pragma unroll                                             // as the storing wave last stored it
+          for (int k = 0; k < 7; k++) {
+            const uint4 v = D.img[ag1][k][l];
+            R.d[4 * k] = v.x; R.d[4 * k + 1] = v.y; R.d[4 * k + 2] = v.z; R.d[4 * k + 3] = v.w;
+          }
+          R.P = unpack_player(D.pl[ag1][l]);
+          R.cells_a = R.cells_n;
+          R.sta = R.stn;
+          R.stn = heads_of(mbits_of(D.heads[na1][l]));
+          R.cells_n = D.cells[na1][l];
+          R.na_active = (D.pl[na1][l].y >> 16) & 0xffu;
+        }
+        if (ended) {                                       // hand the env to k_env_fixup
+          duo_store_env_private<true>(s, i, R);
+          rngs[i] = srng;
+          park = (uint32_t)t | (finish ? kParkFinish : 0u);
+          live = false;
+        }
+        ag = ag1;
+        na = na1;
+      } else {
+        D.ring[t & 1][3][l] = make_uint4(0u, 0u, 0u, 0u);  // no record
+      }
+    }
+    PH(3);
+    __syncthreads();                                       // Y_t
+    PH(4);
+    b3 = b3 == 2 ? 0 : b3 + 1;
+  }
+  __syncthreads();                                         // X_{steps + 1}: every record stored
+  PH_FLUSH(s_glob);
+  if (live) {                                              // env-level private state back to HBM
+    R.flags |= D.sflags[l];                                // (the drawing wave's hazard flags)
+    duo_store_env_private<true>(s, i, R);
+    rngs[i] = srng;
+  } else if (l < ne && D.sflags[l]) {                      // a parked env: flags of its last draws
+    reinterpret_cast<uint32_t *>(s.priv + i)[7] = R.flags | D.sflags[l];
+  }
+  if (l < ne) s.park[i] = park;
+  lds_store_wave<TrioLds, 64>(D, s, 0, ne);                // every player's records (cooperative)
+}
+
+DEV void trio_drawer(TrioLds &D, const DevState &s_glob, int steps) {
+  const int l = (int)threadIdx.x - 64;
+  const size_t wbase = (size_t)blockIdx.x * 64;
+  const DevState s = wave_view(s_glob, wbase);
+  const size_t i = (size_t)l;
+  const bool live = wbase + (size_t)l < s_glob.n;
+  uint32_t rng = live ? reinterpret_cast<const uint32_t *>(s.priv + i)[0] : 0u;   // the env rng
+  D.sflags[l] = 0u;
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();                                         // B
+  PH_DECL;
+  int b3 = 0;
+  for (int t = 0; t <= steps; t++) {
+    __syncthreads();                                       // X_t
+    __syncthreads();                                       // Y_t
+    PH(8);
+    if (t < steps) {                                       // record t's turn ends
+      const uint32_t meta = D.ring[t & 1][3][l].w;
+      const int ag = (int)((meta >> 2) & 3u);
+      const bool te = live && (meta & kMetaValid) && (int)(meta >> 24) != ag;
+      if (__builtin_amdgcn_ballot_w64(te) && te) {
+        uint4 dk[7];
+#pragma unroll
+        for (int k = 0; k < 7; k++) dk[k] = D.deckr[b3][k][l];
+        const uint4 x = D.ring[t & 1][4][l];
+        MBits ba{x.x, x.y, x.z};
+        duo_turn_end(D, l, ag, dk, ba, rng);
+#pragma unroll
+        for (int k = 0; k < 7; k++) D.deckr[b3][k][l] = dk[k];
+        D.ring[t & 1][4][l] = make_uint4(ba.w0, ba.w1, ba.w2, x.w);
+      }
+    }
+    PH(9);
+    b3 = b3 == 2 ? 0 : b3 + 1;
+  }
+  __syncthreads();                                         // X_{steps + 1}
+  if (live) reinterpret_cast<uint32_t *>(s.priv + i)[0] = rng;   // the env rng after its last draws
+  PH_FLUSH(s_glob);
+}
+
+DEV void trio_storer(TrioLds &D, const DevState &s_glob, int steps, uint8_t *__restrict__ actions_glob) {
+  const int l = (int)threadIdx.x - 128;
+  const size_t wbase = (size_t)blockIdx.x * 64;
+  const DevState s = wave_view(s_glob, wbase);
+  const size_t i = (size_t)l;
+  const bool live = wbase + (size_t)l < s_glob.n;
+  uint8_t *__restrict__ av = actions_glob + wbase * COG_ACTION_BYTES;
+  uint4 shb[3];
+  MBits selb = {0u, 0u, 0u}, stb[4];
+  uint32_t out = ~0u;                                      // dones[i] | agent_selection[i] << 8 as stored
+  if (live) {
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+      const uint4 *dk = reinterpret_cast<const uint4 *>(deck_ptr(s, i, p));
+#pragma unroll
+      for (int k = 0; k < 7; k++) D.img[p][k][l] = dk[k];
+    }
+    const uint4 *sh4 = reinterpret_cast<const uint4 *>(s.obs + i * COG_OBS_BYTES + COG_OBS_PHASE);
+#pragma unroll
+    for (int k = 0; k < 3; k++) shb[k] = sh4[k];
+    selb = mbits_of(s.heads[5 * i]);
+#pragma unroll
+    for (int p = 0; p < 4; p++) stb[p] = mbits_of(s.heads[5 * i + 1 + p]);
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();                                         // B: the image is in LDS
+  PH_DECL;
+  int b3 = 2;                                              // (t - 1) % 3
+  for (int t = 0; t <= steps; t++) {
+    __syncthreads();                                       // X_t
+    __syncthreads();                                       // Y_t
+    PH(5);
+    if (t >= 1) {                                          // record t - 1
+      const int rb = (t - 1) & 1;
+      uint4 g[kRingG];
+#pragma unroll
+      for (int k = 0; k < kRingG; k++) g[k] = D.ring[rb][k][l];
+      const uint32_t meta = g[3].w;
+      const bool rec = live && (meta & kMetaValid);
+      const int ag = (int)((meta >> 2) & 3u), na = (int)((meta >> 4) & 3u);
+      if (rec) {
+        uint4 dk[7];
+        uint32_t dm = 0;                                   // deck granules that changed
+#pragma unroll
+        for (int k = 0; k < 7; k++) {
+          dk[k] = D.deckr[b3][k][l];
+          if (ne4(dk[k], D.img[ag][k][l])) dm |= 1u << k;
+        }
+#pragma unroll
+        for (int k = 0; k < 7; k++)
+          if ((dm >> k) & 1u) D.img[ag][k][l] = dk[k];
+        PH(6);
+        uint8_t *ob = s.obs + i * COG_OBS_BYTES;
+        s.info[i * COG_INFO_BYTES + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag] = (uint8_t)(meta >> 8);
+        if (meta & kMetaMoved) reinterpret_cast<uint4 *>(s.priv + i)[2] = g[6];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+          if (ne4(g[k], shb[k])) reinterpret_cast<uint4 *>(ob + COG_OBS_PHASE)[k] = g[k];
+          shb[k] = g[k];
+        }
+        uint8_t *deck = deck_ptr(s, i, ag);
+#pragma unroll
+        for (int k = 0; k < 7; k++)
+          if ((dm >> k) & 1u) reinterpret_cast<uint4 *>(deck)[k] = dk[k];
+        const MBits bs{g[3].x, g[3].y, g[3].z}, ba{g[4].x, g[4].y, g[4].z};
+        store_mask_record(reinterpret_cast<uint4 *>(s.sel + i * COG_MASK_BYTES), bs, mask_diff_granules(bs, selb));
+        selb = bs;
+        store_mask_record(reinterpret_cast<uint4 *>(deck + COG_PD_MASK), ba, mask_diff_granules(ba, selm(stb, ag)));
+        setm(stb, ag, ba);
+        if (na != ag) {
+          const MBits bn{g[5].x, g[5].y, g[5].z};
+          store_mask_record(reinterpret_cast<uint4 *>(deck_ptr(s, i, na) + COG_PD_MASK), bn,
+                            mask_diff_granules(bn, selm(stb, na)));
+          setm(stb, na, bn);
+        }
+        reinterpret_cast<uint2 *>(av + i * COG_ACTION_BYTES)[0] = make_uint2(g[4].w, g[5].w);
+        if (!(meta & kMetaEnded)) {                        // dones[i] = 0, agent_selection[i]
+          const uint32_t agent = meta >> 24;               // (an ended episode: k_env_fixup)
+          if (out & 0xffu) s.done[i] = 0;
+          if (((out >> 8) & 0xffu) != agent) s.agent[i] = (uint8_t)agent;
+          out = agent << 8;
+        }
+      }
+    }
+    PH(13);
+    b3 = b3 == 2 ? 0 : b3 + 1;
+  }
+  __syncthreads();                                         // X_{steps + 1}
+  PH_FLUSH(s_glob);
+}
+
+template <int SRC>
+__global__ void __launch_bounds__(192) k_env_rollout_trio(DevState s, int steps, uint32_t *__restrict__ rngs,
+                                                          uint8_t *__restrict__ actions_out) {
+  __shared__ TrioLds D;
+  const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform
+  uid_tab_fill(D.tab);
+  if (role == 0) {
+    __builtin_amdgcn_s_setprio(3);
+    trio_stepper<SRC>(D, s, steps, rngs);
+  } else if (role == 1) {
+    trio_drawer(D, s, steps);
+  } else {
+    trio_storer(D, s, steps, actions_out);
   }
 }
 
@@ -3538,6 +3918,13 @@ __global__ void __launch_bounds__(256) k_copy_block(const u32x4_t *__restrict__ 
     for (size_t i = base; i < n16; i += 256) cp_st<NT>(cp_ld<NT>(src + i), dst + i);
   }
 }
+// one granule per work-item, a grid covering the buffer (the plain float4 copy of
+// MI355X_MICROARCH.md's measured 6.29 TB/s)
+template <bool NT>
+__global__ void __launch_bounds__(256) k_copy_one(const u32x4_t *__restrict__ src, u32x4_t *__restrict__ dst, size_t n16) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n16) cp_st<NT>(cp_ld<NT>(src + i), dst + i);
+}
 
 // The encode's own read:write mix as a stream (1 granule read, 7 written, all coalesced): the
 // bandwidth an HBM-bound kernel of that mix can reach on this chip, the peak k_encode (16 B of
@@ -3640,35 +4027,59 @@ static void rollout_launch(const DevState &s, int mask_source, int steps, uint32
     hipLaunchKernelGGL((k_env_rollout<MASK_SELECTED, NL>), g, b, 0, st, s, steps, d_rng, d_actions);
 }
 // Which rollout kernels run a shard of n envs (measured on MI355X, device us/step in 1,000-step
-// launches, profiles/r03_rollout_kinds.txt):
+// launches, profiles/r03_rollout_kinds.txt, profiles/r04e_trio_ab.txt):
+//   n <= 32,768, selected masks, >= 3 players: trio (k_env_rollout_trio + k_env_fixup: 1.96 at
+//                8,192 and 16,384, 2.08 at 32,768, against duo 2.45 / pipe 2.75)
 //   n <= 16,384  duo   (k_env_rollout_duo + k_env_fixup: 2.47-2.49 against pipe 2.65-2.68)
 //   n <= 32,768  pipe  (k_env_rollout_pipe: 2.75-2.76 against duo 2.96)
-//   larger       wave  (k_env_rollout: 3.91-3.96 against duo 4.0-4.7)
+//   larger       wave  (k_env_rollout: 3.91-3.96 against duo 4.0-4.7, trio 4.9: its 75 KB of LDS
+//                admit two workgroups per CU, so 1,024 of them run in two rounds)
 // Above 16,384 envs the chip's shader clock drops (2.34 -> 2.08 GHz measured by s_memtime at the
 // same cycles per step), and the duo's storing wave costs more work per env-step than its
-// hand-off saves, so the leaner kernels win there.  $COG_ROLLOUT = duo | pipe | wave forces one.
-enum RolloutKind : int { RK_AUTO = -1, RK_DUO = 0, RK_WAVE = 1, RK_PIPE = 2 };
-static int rollout_kind(size_t n) {
+// hand-off saves, so the leaner kernels win there.  $COG_ROLLOUT = duo | pipe | wave forces one
+// (duo: the trio where it applies; $COG_TRIO=0 keeps the duo).
+enum RolloutKind : int { RK_AUTO = -1, RK_DUO = 0, RK_WAVE = 1, RK_PIPE = 2, RK_TRIO = 3 };
+static bool trio_on() {                                    // $COG_TRIO=0: no trio (A/B)
+  static const bool on = [] {
+    const char *e = getenv("COG_TRIO");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+static int rollout_kind(size_t n, int mask_source, bool defer_ok) {
   static const int forced = [] {
     const char *e = getenv("COG_ROLLOUT");
     if (!e || !*e || !strcmp(e, "auto")) return (int)RK_AUTO;
     return !strcmp(e, "duo") ? (int)RK_DUO : !strcmp(e, "wave") ? (int)RK_WAVE : (int)RK_PIPE;
   }();
-  if (forced != RK_AUTO) return forced;
+  const bool trio = defer_ok && mask_source == MASK_SELECTED && trio_on();
+  if (forced != RK_AUTO) return forced == RK_DUO && trio ? (int)RK_TRIO : forced;
+  if (trio && n <= 32768) return RK_TRIO;
   return n <= 16384 ? RK_DUO : n <= 32768 ? RK_PIPE : RK_WAVE;
 }
-int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions, void *stream) {
+int rollout_kind_of(size_t n, int mask_source, bool defer_ok) { return rollout_kind(n, mask_source, defer_ok); }
+int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions, void *stream,
+                   bool defer_ok) {
   if (!s.n || steps <= 0) return 0;
-  const int kind = rollout_kind(s.n);
-  if (kind == RK_DUO) {
+  const int kind = rollout_kind(s.n, mask_source, defer_ok);
+  if (kind == RK_DUO || kind == RK_TRIO) {
     const hipStream_t st = (hipStream_t)stream;
     const dim3 g(blocks_for(s.n, 64));
+    static const int redo_at = [] {                        // test hook (DevState::redo_at)
+      const char *e = getenv("COG_DEBUG_REDO_STEP");
+      return e && *e ? atoi(e) : -1;
+    }();
+    DevState sd = s;
+    sd.redo_at = redo_at;
     if (mask_source == MASK_STORED) {
-      hipLaunchKernelGGL((k_env_rollout_duo<MASK_STORED>), g, dim3(128), 0, st, s, steps, d_rng, d_actions);
-      hipLaunchKernelGGL((k_env_fixup<MASK_STORED>), g, dim3(64), 0, st, s, steps, d_rng, d_actions);
+      hipLaunchKernelGGL((k_env_rollout_duo<MASK_STORED>), g, dim3(128), 0, st, sd, steps, d_rng, d_actions);
+      hipLaunchKernelGGL((k_env_fixup<MASK_STORED>), g, dim3(64), 0, st, sd, steps, d_rng, d_actions);
+    } else if (kind == RK_TRIO) {                          // selected masks, >= 3 players
+      hipLaunchKernelGGL((k_env_rollout_trio<MASK_SELECTED>), g, dim3(192), 0, st, sd, steps, d_rng, d_actions);
+      hipLaunchKernelGGL((k_env_fixup<MASK_SELECTED>), g, dim3(64), 0, st, sd, steps, d_rng, d_actions);
     } else {
-      hipLaunchKernelGGL((k_env_rollout_duo<MASK_SELECTED>), g, dim3(128), 0, st, s, steps, d_rng, d_actions);
-      hipLaunchKernelGGL((k_env_fixup<MASK_SELECTED>), g, dim3(64), 0, st, s, steps, d_rng, d_actions);
+      hipLaunchKernelGGL((k_env_rollout_duo<MASK_SELECTED>), g, dim3(128), 0, st, sd, steps, d_rng, d_actions);
+      hipLaunchKernelGGL((k_env_fixup<MASK_SELECTED>), g, dim3(64), 0, st, sd, steps, d_rng, d_actions);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
@@ -3718,6 +4129,12 @@ int launch_copy_peak(const void *src, void *dst, size_t bytes, void *stream, int
     const dim3 g(blocks_for(n16, 256)), t(256);
     if (variant & 1) hipLaunchKernelGGL(k_stream_mix<true>, g, t, 0, (hipStream_t)stream, a, b, n16);
     else hipLaunchKernelGGL(k_stream_mix<false>, g, t, 0, (hipStream_t)stream, a, b, n16);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+  if (variant & 16) {                                 // one granule per work-item
+    const dim3 g(blocks_for(n16, 256)), t(256);
+    if (variant & 1) hipLaunchKernelGGL(k_copy_one<true>, g, t, 0, (hipStream_t)stream, a, b, n16);
+    else hipLaunchKernelGGL(k_copy_one<false>, g, t, 0, (hipStream_t)stream, a, b, n16);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
   if (variant & 4) {                                  // one pass, 32 KiB per workgroup

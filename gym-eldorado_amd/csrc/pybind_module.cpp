@@ -330,6 +330,15 @@ PYBIND11_MODULE(_city_of_gold, m) {
     check(cog_device_count(&n));
     return n;
   });
+  m.def(
+      "rollout_kind",
+      [](size_t n, int n_players, bool stored_masks) {
+        static const char *names[] = {"duo", "wave", "pipe", "trio"};
+        const int k = cog_rollout_kind(n, n_players, stored_masks ? 1 : 0);
+        return std::string(k >= 0 && k < 4 ? names[k] : "?");
+      },
+      "n"_a, "n_players"_a = 4, "stored_masks"_a = false,
+      "the persistent rollout kernel launched for a shard of n envs: duo | pipe | wave | trio");
   m.def("default_devices", []() { return default_devices(); },
         "the GPUs a handle created with device=None uses (COG_DEVICES, else COG_DEVICE, else LOCAL_RANK, else 0)");
   m.def(

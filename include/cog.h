@@ -94,6 +94,12 @@ typedef struct cog_env_views {
 COG_API const char *cog_last_error(void);
 COG_API int cog_abi_version(void);
 COG_API int cog_device_count(int *out);
+/* which persistent rollout kernel cog_runner_rollout launches for a shard of n envs with
+ * n_players players, sampling the selected (stored_masks 0) or stored masks (measurement labels
+ * only): 0 duo (k_env_rollout_duo + k_env_fixup), 1 wave (k_env_rollout), 2 pipe
+ * (k_env_rollout_pipe), 3 trio (k_env_rollout_trio + k_env_fixup); $COG_ROLLOUT / $COG_TRIO
+ * force one (cog_engine.hip rollout_kind) */
+COG_API int cog_rollout_kind(size_t n_envs, int n_players, int stored_masks);
 
 /* ---- vectorized environment ------------------------------------------------------------ */
 /* vec_cog_env<N>() (vec_environment.h:23-30): N default-constructed envs on `device`;

@@ -175,19 +175,23 @@ def test_full_dynamics_beyond_4gib_of_observations(cg):
     assert np.array_equal(got["agent_selection"], orc.agent_selection)
 
 
-@pytest.mark.parametrize("n", [24576, 4096], ids=["pipe_24576", "duo_4096"])
-@pytest.mark.parametrize("stored", [True, False], ids=["stored_masks", "selected_masks"])
-def test_episode_ends_in_the_two_wave_rollouts(cg, n, stored):
-    """Batches of 16,385-32,768 envs run the two-wave pipe rollout, smaller ones the duo
-    (rollout_kind): episode ends inside their launches go to the fix-up pass (in the pipe kernel,
-    after the storing wave's last stores; k_env_fixup after the duo), which completes them
-    (finish, auto-reset with map generation) and runs the env's remaining steps.  Episodes of 30
-    turns, so most envs end inside the launches; the first and the last 128 envs against
-    1-env-seeded oracle batches."""
-    seed, steps = (777 if stored else 778) + n, 150
+@pytest.mark.parametrize("n", [24576, 4096], ids=["n24576", "n4096"])
+@pytest.mark.parametrize("stored,players", [(True, 4), (False, 4), (False, 2), (False, 3)],
+                         ids=["stored_4p", "selected_4p", "selected_2p", "selected_3p"])
+def test_episode_ends_in_the_two_wave_rollouts(cg, n, stored, players):
+    """The multi-wave rollouts by rollout_kind: 16,385-32,768 envs run the two-wave pipe, smaller
+    batches the duo, and with the selected masks and >= 3 players both sizes run the trio (its
+    deferred turn end).  Episode ends inside their launches go to the fix-up pass (in the pipe
+    kernel, after the storing wave's last stores; k_env_fixup after the duo and the trio), which
+    completes them (finish, auto-reset with map generation) and runs the env's remaining steps.
+    Episodes of 30 turns, so most envs end inside the launches; the first and the last 128 envs
+    against 1-env-seeded oracle batches."""
+    want = "trio" if not stored and players >= 3 else ("pipe" if n > 16384 else "duo")
+    assert cg._city_of_gold.rollout_kind(n, players, stored) == want
+    seed, steps = (777 if stored else 778) + n + 10 * players, 150
     env = cg.vec.get_vec_env(n)()
     smp = cg.vec.get_vec_sampler(n)(seed)
-    env.reset(seed, 4, 3, cg.MEDIUM, 30, False)
+    env.reset(seed, players, 3, cg.MEDIUM, 30, False)
     runner = cg.vec.get_runner(n)(env, smp, None, device_views=True, stored_masks=stored)
     runner.set_chunk(50)
     runner.rollout(steps)
@@ -195,11 +199,11 @@ def test_episode_ends_in_the_two_wave_rollouts(cg, n, stored):
     env.sync_host()
     for lo, hi in ((0, 128), (n - 128, n)):
         orc, osm = po.OracleVec(hi - lo), po.OracleSampler(hi - lo, seed + lo)
-        orc.reset(seed + lo, 4, 3, 1, 30)
+        orc.reset(seed + lo, players, 3, 1, 30)
         resets = 0
         for _ in range(steps):
             osm.sample(po.stored_masks(orc) if stored else orc.selected_action_masks)
             orc.step(osm.actions)
             resets += int(orc.dones.sum())
         assert resets > 0, "no episode ended inside the launches"
-        assert_equal(env, orc, lo, hi, what=f"{n}-env rollout envs [{lo}, {hi}) ({'stored' if stored else 'selected'})")
+        assert_equal(env, orc, lo, hi, what=f"{n}-env {want} rollout envs [{lo}, {hi}) ({'stored' if stored else 'selected'}, {players}p)")

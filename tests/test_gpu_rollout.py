@@ -119,3 +119,52 @@ def test_rollout_zero_steps_and_empty_batch(cg):
     r0.set_chunk(8)
     r0.rollout(20)
     r0.sync()
+
+
+REDO_SCRIPT = r'''
+import sys
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import numpy as np
+import city_of_gold as cg
+import pyoracle as po
+n, seed, steps = int(sys.argv[3]), 4242, 60
+env = cg.vec.get_vec_env(n)(device=0)
+smp = cg.vec.get_vec_sampler(n)(seed, device=0)
+env.reset(seed, 4, 3, cg.HARD, int(sys.argv[4]), False)
+run = cg.vec.get_runner(n)(env, smp, None, device_views=True)
+run.set_chunk(20)
+run.rollout(steps)
+run.sync()
+env.sync_host()
+orc, osm = po.OracleVec(n), po.OracleSampler(n, seed)
+orc.reset_threaded(seed, 4, 3, 2, int(sys.argv[4]))
+po.run_threaded(orc, osm, steps, po.host_threads())
+for nm in ("observations", "selected_action_masks", "infos"):
+    bad = po.named_equal(getattr(env, nm), getattr(orc, nm))
+    assert bad is None, f"{nm}.{bad} differs from the oracle"
+for nm in ("rewards", "dones", "agent_selection"):
+    assert np.array_equal(getattr(env, nm), getattr(orc, nm)), nm
+print("OK", int(orc.infos["total_length"].astype(bool).sum()))
+'''
+
+
+@pytest.mark.parametrize("max_steps", [100000, 12])
+def test_trio_deferred_turn_end_redo_path(cg, tmp_path, max_steps):
+    """The trio rollout's deferred turn end (selected masks, >= 3 players: the drawing wave runs the
+    turn end's discard + draws with the env rng) parks an env whose action would draw from the env
+    rng inside a step (kParkRedo), and k_env_fixup runs that step and the rest with the full step.
+    The canonical loop never takes such an action, so the test hook COG_DEBUG_REDO_STEP=7 parks
+    every env at step 7 of each 20-step launch; 4,096 envs (the trio) against the oracle, with and
+    without episode ends (max_steps 12: parks for finished episodes in the same launches)."""
+    import os
+    import subprocess
+    import sys
+    assert cg._city_of_gold.rollout_kind(4096) == "trio"
+    pkg = os.path.dirname(os.path.dirname(cg.__file__))
+    oracle_dir = os.path.join(os.path.dirname(pkg), "oracle")
+    script = tmp_path / "redo.py"
+    script.write_text(REDO_SCRIPT)
+    r = subprocess.run([sys.executable, str(script), pkg, oracle_dir, "4096", str(max_steps)], capture_output=True,
+                       text=True, timeout=240, env=dict(os.environ, COG_DEBUG_REDO_STEP="7"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.strip().splitlines()[-1].startswith("OK")

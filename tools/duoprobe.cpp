@@ -54,7 +54,11 @@ int main(int argc, char **argv) {
     fflush(stdout);
 #ifdef COG_STAMPS
     {
-      const size_t waves = 2 * ((n + 63) / 64);
+      // the duo: 2 waves per workgroup (stepping, storing); the trio ($COG_TRIO unset): 3 (stepping,
+      // drawing, storing).  Each wave's PH slots (cog_engine.hip): its own phase names below.
+      const char *trio_env = getenv("COG_TRIO");
+      const int wpg = (trio_env && *trio_env == '0') ? 2 : 3;
+      const size_t waves = (size_t)wpg * ((n + 63) / 64);
       constexpr int K = 16;
       unsigned long long *d;
       if (hipMalloc(&d, waves * K * sizeof(unsigned long long)) != hipSuccess) return 1;
@@ -67,20 +71,28 @@ int main(int argc, char **argv) {
       env->sh[0].s.stamps = nullptr;
       std::vector<unsigned long long> h(waves * K);
       if (hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return 1;
-      const char *pn[16] = {"S: step tail (done check)", "S: LDS player writes", "S: wait X", "S: ring write + turn change",
-                            "S: wait Y", "W: wait Y", "W: ring read, images, slot", "W: wait X",
-                            "S: sample + action branch", "S: mip + end_turn discard", "S: draw", "S: mask swap, sh, cells",
-                            "S: update_observation", "W: stores", "", ""};
-      double tot[2] = {0, 0};
-      for (int k = 0; k < 14; k++) {
-        const int role = pn[k][0] == 'S' ? 0 : 1;
-        std::vector<double> v;
-        for (size_t w = role; w < waves; w += 2) v.push_back((double)h[w * K + k] / chunk);
-        const double m = med(v);
-        tot[role] += m;
-        printf("  %-36s %8.0f\n", pn[k], m);
+      const char *step_names[16] = {"step tail (done check)", "LDS player writes", "wait X", "ring write + turn change",
+                                    "wait Y", "", "", "", "sample + action branch", "mip + end_turn discard",
+                                    "draw", "mask swap, sh, cells", "update_observation", "", "", ""};
+      const char *store_names[16] = {"", "", "", "", "", "wait Y", "ring read, images, slot", "wait X", "", "", "",
+                                     "", "", "stores", "", ""};
+      const char *draw_names[16] = {"", "", "", "", "", "", "", "", "wait X, Y", "turn-end draws", "", "", "", "", "",
+                                    ""};
+      const char *role_name[3] = {"stepping", wpg == 3 ? "drawing" : "storing", "storing"};
+      for (int role = 0; role < wpg; role++) {
+        const char **pn = role == 0 ? step_names : (wpg == 3 && role == 1) ? draw_names : store_names;
+        double tot = 0;
+        printf("  %s wave:\n", role_name[role]);
+        for (int k = 0; k < 16; k++) {
+          if (!pn[k][0]) continue;
+          std::vector<double> v;
+          for (size_t w = role; w < waves; w += wpg) v.push_back((double)h[w * K + k] / chunk);
+          const double m = med(v);
+          tot += m;
+          printf("    %-34s %8.0f\n", pn[k], m);
+        }
+        printf("    %-34s %8.0f  (ticks per step)\n", "sum", tot);
       }
-      printf("  stepping wave sum %8.0f   storing wave sum %8.0f  (ticks per step)\n", tot[0], tot[1]);
       (void)hipFree(d);
     }
 #endif

@@ -1,9 +1,9 @@
 #!/bin/bash
 # PMC passes over the benchmark workload (bench.py --profile-steps K): each counter group in its
 # own rocprofv3 run with --kernel-trace only (never combined with sys/runtime traces), then a
-# per-kernel summary.   Usage (on the GPU box): tools/pmc_passes.sh TAG [K] [chunk]
+# per-kernel summary.   Usage (on the GPU box): tools/pmc_passes.sh TAG [K] [chunk] [envs]
 set -o pipefail
-TAG=${1:-pmc}; STEPS=${2:-2000}; CHUNK=${3:-1000}
+TAG=${1:-pmc}; STEPS=${2:-2000}; CHUNK=${3:-1000}; ENVS=${4:-65536}
 OUT=$PWD/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -11,7 +11,7 @@ BENCH="$PWD/bench.py"
 run() {   # name, counters...
   local name=$1; shift
   (cd /tmp && timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d "$OUT/$name" -o run \
-      --pmc "$@" -- python3 "$BENCH" --profile-steps "$STEPS" --chunk "$CHUNK" --warmup 0 --no-cpu-baseline) \
+      --pmc "$@" -- python3 "$BENCH" --profile-steps "$STEPS" --chunk "$CHUNK" --envs-total "$ENVS" --warmup 0 --no-cpu-baseline) \
       > "$OUT/$name.log" 2>&1
 }
 run sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS && \

@@ -6,7 +6,7 @@ SQ_*_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles.  Writes profiles/p
 stamped with the hash of the engine source so that bench.py uses it only for the kernel version
 it measures.
 
-    python tools/pmc_profile.py <dir of the K-step capture>:<K> [<dir>:<K> ...]  [--envs 65536]
+    python tools/pmc_profile.py <dir of the K-step capture>:<K>[:<envs>] [<dir>:<K>[:<envs>] ...]  [--envs 65536]
                                 [--coeff <tools/store_coeff.sh output dir> | --coeff keep]
 
 The first capture gives the per-wave-step instruction and cycle counts (use a long K); every
@@ -72,17 +72,67 @@ def store_costs(d):
                     "from both"}
 
 
+ROLLOUT_ANY = "void cog::k_env_rollout"                 # wave, pipe and duo kernels
+COMPANION = "void cog::k_env_fixup"                    # the duo's fix-up launch (same batch)
+
+
+def kind_of(name):
+    return "duo" if "_duo" in name else "trio" if "_trio" in name else "pipe" if "_pipe" in name else "wave"
+
+
+def rollout_entry(res, envs, k):
+    """The rollout kernel of one capture (the one with the most dispatches x duration is the only
+    k_env_rollout* name in a capture of one shard size): counter HBM bytes, L2 writes / hits /
+    misses and per-wave-step issue counts, per launch of k steps over `envs` envs."""
+    names = [n for n in res if n.startswith(ROLLOUT_ANY)]
+    if not names:
+        return None
+    name = names[0]
+    r = res[name]
+    waves = (envs + 63) // 64                           # stepping waves (the duo / pipe: one per 64 envs)
+    per = lambda c: r[c] / waves / k if c in r else None   # noqa: E731
+    e = {"kernel": name, "kind": kind_of(name), "envs": envs, "chunk": k, "dispatches": r["dispatches"],
+         "bytes_per_launch": traffic(r)}
+    comp = next((v for n, v in res.items() if n.startswith(COMPANION)), None)
+    if comp is not None and traffic(comp) is not None:
+        e["companion"] = {"kernel": COMPANION, "bytes_per_launch": traffic(comp)}
+    if "TCC_WRITE_sum" in r and "TCC_HIT_sum" in r:
+        e["l2_per_launch"] = {"writes": r["TCC_WRITE_sum"], "hits": r["TCC_HIT_sum"], "misses": r["TCC_MISS_sum"],
+                              "fabric_write_requests": r.get("TCC_EA0_WRREQ_sum")}
+    if "SQ_INSTS_VALU" in r:
+        e["per_wave_step"] = {"note": "counts over every wave of the launch (stepping and storing waves) / "
+                                      "(envs / 64) / steps",
+                              "valu": per("SQ_INSTS_VALU"), "salu": per("SQ_INSTS_SALU"), "lds": per("SQ_INSTS_LDS"),
+                              "vmem_wr": per("SQ_INSTS_VMEM_WR"), "active_inst_any": per("SQ_ACTIVE_INST_ANY"),
+                              "wait_any": per("SQ_WAIT_ANY"), "wave_cycles": per("SQ_WAVE_CYCLES")}
+    if e["bytes_per_launch"] is not None:
+        e["bytes_per_env_step"] = e["bytes_per_launch"] / envs / k
+    return e
+
+
 def main(specs, envs=65536, coeff=None):
+    """specs: <capture dir>:<K>[:<envs>] -- the first spec at the default envs gives the legacy
+    `k_env_rollout` block (per-wave-step counts of the N=1 kernel) and the k_env_step / k_encode
+    figures; every spec adds a `rollouts` entry keyed "<envs>:<K>" (the bench's roofline at any
+    shard size takes the entry of its own launch shape, or none)."""
     waves = (envs + 63) // 64
     out = {"engine_sha": engine_hash(), "sources": specs,
            "method": "bytes = 2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024 (gfx950 corrections), mean per "
                      "dispatch; per-wave-step counts = counter / waves / steps per launch"}
     ro = {"envs_per_launch": envs, "bytes_per_step_launch": {}}
-    for j, spec in enumerate(specs):
-        d, k = spec.rsplit(":", 1)
-        k = int(k)
+    rollouts = {}
+    first = True
+    for spec in specs:
+        parts = spec.split(":")
+        d, k = parts[0], int(parts[1])
+        n = int(parts[2]) if len(parts) > 2 else envs
         res = summary(d)
-        r = next((v for k, v in res.items() if k.startswith(ROLLOUT)), None)
+        e = rollout_entry(res, n, k)
+        if e:
+            rollouts[f"{n}:{k}"] = e
+        if n != envs:
+            continue
+        r = next((v for kk, v in res.items() if kk.startswith(ROLLOUT)), None)
         if r:
             b = traffic(r)
             if b is not None:
@@ -91,7 +141,7 @@ def main(specs, envs=65536, coeff=None):
                 ro.setdefault("l2_per_launch", {})[str(k)] = {
                     "writes": r["TCC_WRITE_sum"], "hits": r["TCC_HIT_sum"], "misses": r["TCC_MISS_sum"],
                     "fabric_write_requests": r.get("TCC_EA0_WRREQ_sum")}
-            if j == 0:
+            if first:
                 per = lambda c: r[c] / waves / k if c in r else None   # noqa: E731
                 ro.update(steps_per_launch=k, valu_per_wave_step=per("SQ_INSTS_VALU"),
                           salu_per_wave_step=per("SQ_INSTS_SALU"), lds_per_wave_step=per("SQ_INSTS_LDS"),
@@ -102,7 +152,7 @@ def main(specs, envs=65536, coeff=None):
                           per_env_step=(b / envs / k) if b is not None else None,
                           l2_hit=r.get("TCC_HIT_sum", 0) / max(1.0, r.get("TCC_HIT_sum", 0) + r.get("TCC_MISS_sum", 0)),
                           gui_active=r.get("GRBM_GUI_ACTIVE"))
-        if j == 0:
+        if first:
             for name, short in ((STEP, "k_env_step"), (ENCODE, "k_encode")):
                 kk = res.get(name)
                 if kk:
@@ -113,7 +163,9 @@ def main(specs, envs=65536, coeff=None):
                         out[short]["l2_per_launch"] = {"writes": kk.get("TCC_WRITE_sum"), "hits": kk["TCC_HIT_sum"],
                                                        "misses": kk["TCC_MISS_sum"],
                                                        "fabric_write_requests": kk.get("TCC_EA0_WRREQ_sum")}
+        first = False
     out["k_env_rollout"] = ro
+    out["rollouts"] = rollouts
     if coeff == "keep":                     # the store costs are the probe's, not the engine's: carry them over
         with open(os.path.join(ROOT, "profiles", "pmc_profile.json")) as f:
             prev = json.load(f).get("store_costs")
