@@ -1438,6 +1438,41 @@ DEV void sample_heads(const Heads &h, uint32_t &rng, uint8_t out[5], const UidEn
       if (k[j] >= 2u) out[j] = (uint8_t)nth_set_bit(m[j], uid_tab(tab, r[j], k[j]));
   }
 }
+// The trio's presampled draws.  With every head non-empty a sample takes exactly five accepted
+// draws, so the sampler's state two steps on is known before those steps run: the storing wave
+// computes, from the state a step record carries, the five draws of the step after next
+// (presample: the state they start from, head 0's draw, the state after the five, and whether any
+// draw could be rejected) and the stepping wave samples from them (sample_presampled) when its
+// state is the one they start from and every head is non-empty -- else, or when a head other than
+// head 0 holds two or more candidates, it draws the sequential way (sample_heads).  The values
+// are the same either way (cog_rng.h jump-ahead: x * 16807^j mod (2^31 - 1)).
+constexpr uint32_t kPow5 = mr_pow(5), kPow10 = mr_pow(10), kPow15 = mr_pow(15);
+DEV uint4 presample(uint32_t x) {                          // x: the state the step starts from
+  uint32_t y = x, r0 = 0, risk = 0;
+#pragma unroll
+  for (int j = 0; j < 5; j++) {
+    const uint32_t r = mr_next(y) - 1u;
+    if (j == 0) r0 = r;
+    risk |= r >= kSmallSafe ? 1u : 0u;
+  }
+  return make_uint4(x, r0, y, risk);
+}
+// act[0..4] from the presampled draws; false: not applicable (the caller samples sequentially)
+DEV bool sample_presampled(const Heads &h, const uint4 &pre, uint32_t &rng, uint8_t out[5], const UidEntry *tab) {
+  const uint32_t m[5] = {h.play, h.spec, h.rem, h.move, h.shop};
+  bool ok = pre.x == rng && pre.w == 0u;
+#pragma unroll
+  for (int j = 1; j < 5; j++) ok = ok && __popc(m[j]) == 1;  // heads 1-4: one candidate each
+  const uint32_t k0 = __popc(m[0]);
+  ok = ok && k0 >= 1u;
+  if (!ok) return false;
+  const UidEntry e0 = tab[k0];
+  out[0] = (uint8_t)(k0 >= 2u ? nth_set_bit(m[0], uid_tab_accepted(pre.y, e0.s, e0.m)) : (uint32_t)(__ffs(m[0]) - 1));
+#pragma unroll
+  for (int j = 1; j < 5; j++) out[j] = (uint8_t)(__ffs(m[j]) - 1);
+  rng = pre.z;
+  return true;
+}
 DEV void sample_mask(const uint8_t *mask, uint32_t &rng, uint8_t out[5], const UidEntry *tab) {
   sample_heads(heads_of(mbits_from_bytes(mask)), rng, out, tab);
 }
@@ -2006,10 +2041,6 @@ DEV void dup_sink(const RegEnv &R2) {
 }
 #endif
 
-// DEFER (the trio rollout's deferred turn end): the turn end's discard and draws are left to the
-// drawing wave (trio_drawer), which owns the env rng -- the acting player's counters (n_active =
-// 0) and the saved mask (the selected mask before the draws) go out as they stand.
-template <bool DEFER = false>
 DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i, int na PH_PARAM) {
   const int ag = (int)R.agent();
   PState &P = R.P;
@@ -2174,7 +2205,7 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
 #endif
     P.n_active = 0;                                        // Player::end_turn (player.cpp:170-180)
     PH(9);
-    if (!DEFER) R.end_turn_deck();
+    R.end_turn_deck();
     PH(10);
     R.sta = R.sel;                                         // save_actionmask
     R.set_agent((uint32_t)na);
@@ -2222,6 +2253,63 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
     return false;
   }
   const uint32_t c0 = R.use_cell(cc, 0);                   // done check (:187)
+  return COG_HEX_END(c0) || R.turn_counter >= R.max_steps;
+}
+
+// The trio's step (k_env_rollout_trio): cog_env::step (environment.cpp:91-224) for an action that
+// plays a card or passes, by a player with no move, free card, free move or pending removes in
+// progress and who has not won (lean_ok) -- every step of the canonical selected-mask loop
+// (SURVEY Q1); any other env is parked before its step (kParkRedo) and run by the full step.
+// Three parts of the reference's step are left to the other waves: the deck's piles other than the
+// hand (the drawing wave replays the play on its copy of the deck, trio_drawer), the turn end's
+// discard + draws (the drawing wave too) and update_observation's movement / shop heads of the acting
+// player's stored mask when the turn goes on -- with the selected masks nothing reads those
+// heads but the output record (save_actionmask replaces them at the turn end), so the storing
+// wave computes them from the step record (trio_storer).  At a turn end the new agent's stored
+// mask gets update_observation's values for the INACTIVE phase (move = shop = {0}) here.
+DEV bool lean_ok(const RegEnv &R, const uint8_t act[5]) {
+  return ((uint32_t)act[1] | act[2] | act[3] | act[4] | R.P.next_move_free | R.P.next_card_free | R.P.n_removes |
+          R.P.mip | R.P.has_won) == 0u;
+}
+DEV bool step_lean(RegEnv &R, int a_play, int na, bool &turn_end) {   // (R.d: the hand pile only)
+  const int ag = (int)R.agent();
+  PState &P = R.P;
+  const uint32_t info = ((R.info_steps >> (8 * ag)) + 1u) & 0xffu;   // Info steps_taken (u8)
+  R.info_steps = (R.info_steps & ~(0xffu << (8 * ag))) | (info << (8 * ag));
+  uint32_t phase = R.sh[0] & 0xffu;
+  if (phase == COG_PHASE_INACTIVE) phase = COG_PHASE_MOVEMENT;
+  P.steps_taken = (P.steps_taken + 1) & 0xffu;
+  float r0 = __uint_as_float(R.sh[1]), r1 = __uint_as_float(R.sh[2]), r2 = __uint_as_float(R.sh[3]);
+  if (a_play > 8) P.pad = 1u;                              // the deck's "wide" flag (step_regs)
+  if (a_play) {                                            // Player::play_card (player.cpp:45-60)
+    const int c = a_play - 1;
+    if (phase == COG_PHASE_MOVEMENT) {
+      r0 = (float)cardf(kRes0, c); r1 = (float)cardf(kRes1, c); r2 = (float)cardf(kRes2, c);
+    } else if (phase == COG_PHASE_BUYING) {
+      const uint32_t coin = cardf(kRes2, c);
+      r2 = r2 + (coin > 0 ? (float)coin : 0.5f);
+    }
+    R.leave_hand(c, false);                                // Deck::activate (the active pile: the
+    P.n_active = (P.n_active + 1) & 0xffu;                 // drawing wave replays it, trio_drawer)
+    P.idx_last = (uint32_t)c;
+  } else {
+    phase = (phase + 1) % 3;                               // pass: next phase
+  }
+  turn_end = phase == COG_PHASE_INACTIVE;                  // maybe_end_turn -> next_agent
+  if (turn_end) {
+    P.n_active = 0;                                        // Player::end_turn (the deck: drawing wave)
+    R.sta = R.sel;                                         // save_actionmask
+    R.set_agent((uint32_t)na);
+    R.sel = R.stn;                                         // load_actionmask (na != ag: >= 3 players)
+    R.stn.move = 1u;                                       // update_observation, INACTIVE phase
+    R.stn.shop = 1u;
+    r0 = r1 = r2 = 0.f;
+    R.turn_counter++;
+  }
+  R.sh[0] = (R.sh[0] & ~0xffu) | phase;
+  R.sh[1] = __float_as_uint(r0); R.sh[2] = __float_as_uint(r1); R.sh[3] = __float_as_uint(r2);
+  const uint2 cc = turn_end ? R.cells_n : R.cells_a;      // (a copy: a reference picked between two
+  const uint32_t c0 = R.use_cell(cc, 0);                   // members would keep R out of registers)
   return COG_HEX_END(c0) || R.turn_counter >= R.max_steps;
 }
 
@@ -3105,6 +3193,7 @@ static_assert(sizeof(DuoLds) <= 40960, "four duo workgroups per CU");
 // acting player), 8-15 Info steps byte of ag, 16 the episode ended (parked: dones / agent are
 // left to the fix-up), 24-31 agent after the step
 constexpr uint32_t kMetaValid = 1u, kMetaMoved = 2u, kMetaEnded = 1u << 16;
+constexpr uint32_t kMetaStepped = 1u << 17;               // (trio) the step ran: the env was not done
 
 DEV uint32_t next_player(uint32_t a, uint32_t np) { return a + 1u >= np ? 0u : a + 1u; }
 
@@ -3432,33 +3521,63 @@ __global__ void __launch_bounds__(128) k_env_rollout_duo(DevState s, int steps, 
 }
 
 // ------------------------------------------------------------------------------------------
-// Trio rollout (round 4): the duo with the turn end's discard + draws deferred to a wave of their
-// own, for the selected-mask loop with >= 3 players on shards of <= 16,384 envs.  Tried first with
-// the duo's two waves, the storing wave doing the draws (profiles/r04d_duo_defer.txt, 8,192
-// envs): deferring cut the stepping wave's work from 6,340 to 5,040 ticks per step, but the
-// storing wave then carried its stores (2,790) and the draws (2,100) and set the pace at 7,900 --
-// so the draws go to a third wave, and the storing wave's deck image moves to LDS (the stepping
-// wave takes the next agent's deck straight from it: no per-step hand-over copy).
+// Trio rollout (round 4): the selected-mask loop with >= 3 players on shards of <= 32,768 envs,
+// one step's work spread over four waves per 64 envs.  The stepping wave runs the lean step
+// (step_lean: sample, play or pass, turn change, done check) and nothing else; the drawing wave
+// owns the decks (replays each play on its copy, runs the turn ends' discard + draws with the env
+// rng); two storing waves issue the store phase, one of them also producing the sampler's
+// presampled draws (presample).  History (8,192 envs, device us per step in 1,000-step launches,
+// profiles/r04*_trio*.txt): the duo 2.45; its storing wave doing the draws 3.17 (it set the pace,
+// profiles/r04d_duo_defer.txt); the draws on a third wave 1.96; lean step, hand-only stepping
+// wave, presampled draws and two storing waves 1.80; turn ends batched over two records (below).
 //
-// Per step t the stepping wave writes record t (ring[t & 1], deckr[t % 3]); the drawing wave
-// completes record t's turn ends in [Y_t, X_{t+1}] (the env rng is its own: it rewrites the
-// record's deck and saved mask in place, and the player's counters and stored-mask bits in
-// pl / heads); the storing wave stores record t one step later, in [Y_{t+1}, X_{t+2}], and updates
-// the deck image.  The loop runs steps + 1 rounds (the last drains the pipeline), then one more
-// barrier; every wave executes every barrier.  Why the reads are safe: the stepping wave reads a
-// player's deck image, counters or stored mask only when that player is the next agent or the one
-// after it, and with >= 3 players every turn end of that player lies at least two steps back --
-// its record is through both waves by then (the deferred turn end note above step_draws_rng).
+// Pipeline, per step t (barriers X_t, Y_t; every wave executes every barrier):
+//   stepping wave  [Y_{t-1}, X_t] step t;  [X_t, Y_t] record t -> ring[t % 3], turn change
+//   drawing wave   at odd t, [Y_t, X_{t+1}]: records t - 1 and t -- the plays replayed on the
+//                  acting players' decks (img), then ONE turn-end pass: a lean turn lasts at least
+//                  two steps (pass in MOVEMENT, pass in BUYING), so a player ends at most one turn
+//                  in two records, and the pass runs once per two steps
+//   storing waves  [Y_{t+2}, X_{t+3}] record t (ring, deckr / dmask from the drawing wave)
+// The loop runs steps + 2 rounds (the last two drain the pipeline), then one more barrier.  Why
+// the stepping wave's reads are safe: it reads a player's hand (img), counters (pl) or stored mask
+// (heads) only when that player becomes the agent or the one after it, and with >= 3 players and
+// turns of >= 2 steps, that player's last turn end lies >= 2 steps back: the drawing wave finished
+// it by then (X_{t_e + 2}).
+//
+// record t: 0 ObsData 16128.. (phase, resources; the lean step never changes the shop), 1 selected-
+// mask bits + meta, 2 the acting player's stored-mask bits (saved mask at a turn end: the drawing
+// wave adds the drawn cards) + action byte 0, 3 the next player's stored-mask bits + n_active of
+// the acting player << 8.  The neighbourhood caches never change in the lean step (no moves): the
+// stepping wave and storing wave A keep their own copies, and the epilogue does not store them.
+constexpr int kTrioRingG = 4;
 struct TrioLds {
-  uint4 img[4][7][64];                // every player's DeckObs as last stored (the storing wave's image)
-  uint4 deckr[3][7][64];              // record t's DeckObs (acting player after the step), t % 3
-  uint4 ring[2][kRingG][64];          // record t (duo layout), t & 1
+  uint4 img[4][7][64];                // every player's DeckObs (the drawing wave's)
+  uint4 deckr[3][7][64];              // record t's DeckObs granules that changed, t % 3
+  uint32_t dmask[3][64];              // ... which ones
+  uint4 ring[3][kTrioRingG][64];      // record t (above), t % 3
+  uint32_t srng[3][64];               // the sampler state after step t, t % 3
+  uint4 pre[2][64];                   // presampled draws of step t (storing wave B), t & 1
   uint4 pl[4][64];
-  uint2 cells[4][64];
   uint4 heads[4][64];
   uint32_t sflags[64];                // hazard flags of the drawing wave's draws
+  uint32_t wflags[64];                // ... and of storing wave A's update_observation
   UidEntry tab[kUidTab];
 };
+static_assert(sizeof(TrioLds) <= 75520, "two trio workgroups per CU (measured: 78,336 B admit one)");
+
+DEV int mod3_next(int c) { return c == 2 ? 0 : c + 1; }
+DEV int mod3_prev(int c) { return c == 0 ? 2 : c - 1; }
+
+// the epilogue's player records (lds_store_wave without the neighbourhood caches)
+DEV void trio_store_players(const TrioLds &D, const DevState &s, int ne) {
+  const int l = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int f = j * 64 + l, e = min(f >> 2, ne - 1), q = f & 3;
+    reinterpret_cast<uint4 *>(s.priv + e)[4 + q] = D.pl[q][e];
+    s.heads[5 * e + 1 + q] = D.heads[q][e];
+  }
+}
 
 template <int SRC>
 DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, uint32_t *__restrict__ rngs_glob) {
@@ -3471,6 +3590,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, uint32_t *_
   bool live = l < ne;
   uint32_t park = kParkNone, srng = 0;
   RegEnv R;
+  uint2 cells[4];                                          // every player's neighbourhood cache
   int ag = 0, na = 0;
   if (live) {
     Snap S;
@@ -3480,7 +3600,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, uint32_t *_
 #pragma unroll
     for (int p = 0; p < 4; p++) {
       D.pl[p][l] = pv4[4 + p];
-      D.cells[p][l] = reinterpret_cast<const uint2 *>(pv4 + 8)[p];
+      cells[p] = reinterpret_cast<const uint2 *>(pv4 + 8)[p];
       D.heads[p][l] = s.heads[5 * i + 1 + p];
     }
     srng = rngs[i];
@@ -3488,52 +3608,55 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, uint32_t *_
     na = (int)next_player((uint32_t)ag, R.n_players());
     R.P = unpack_player(D.pl[ag][l]);
     R.na_active = (D.pl[na][l].y >> 16) & 0xffu;
-    R.cells_a = D.cells[ag][l];
-    R.cells_n = D.cells[na][l];
+    uint2 ca = cells[3], cn = cells[3];                    // (selects: no indexed registers)
+#pragma unroll
+    for (int p = 2; p >= 0; p--) {
+      ca = ag == p ? cells[p] : ca;
+      cn = na == p ? cells[p] : cn;
+    }
+    R.cells_a = ca;
+    R.cells_n = cn;
     R.sta = heads_of(mbits_of(D.heads[ag][l]));
     R.stn = heads_of(mbits_of(D.heads[na][l]));
   }
   R.tab = D.tab;
   __builtin_amdgcn_s_waitcnt(0);                           // (no per-iteration vmcnt wait covers them)
-  __syncthreads();                                         // B: the storing wave loaded every deck
-  if (live) {
+  __syncthreads();                                         // B: the drawing wave loaded every deck
 #pragma unroll
-    for (int k = 0; k < 7; k++) {
+  for (int k = 0; k < 28; k++) R.d[k] = 0u;                // (only the hand pile is the stepping wave's:
+  if (live) {                                              // bytes 21..41, granules 1 and 2)
+#pragma unroll
+    for (int k = 1; k < 3; k++) {
       const uint4 v = D.img[ag][k][l];
       R.d[4 * k] = v.x; R.d[4 * k + 1] = v.y; R.d[4 * k + 2] = v.z; R.d[4 * k + 3] = v.w;
     }
   }
   PH_DECL;
-  int b3 = 0;                                              // t % 3
-  for (int t = 0; t <= steps; t++) {
-    bool ended = false, finish = false;
+  int c3 = 0;                                              // t % 3
+  for (int t = 0; t <= steps + 1; t++) {
+    bool ended = false, finish = false, turn_end = false, stepped = false;
     uint8_t act[5];
     if (t < steps && live) {
       const uint32_t srng0 = srng;
-      step_action<SRC>(R, make_uint2(0u, 0u), srng, act);
-      bool redo = false;
-      const bool rare = !act[0] && (act[1] | act[3]) != 0;
-      if (__builtin_amdgcn_ballot_w64(rare) && rare) redo = step_draws_rng(R, act);
-      redo = redo || t == s.redo_at;                       // (test hook, -1: off)
-      if (redo) {                                          // hand the env to k_env_fixup, step t not run
+      const bool fast = sample_presampled(R.sel, D.pre[t & 1][l], srng, act, R.tab);
+      if (__builtin_amdgcn_ballot_w64(!fast) && !fast)     // (wave-uniform skip)
+        step_action<SRC>(R, make_uint2(0u, 0u), srng, act);
+      const bool was_done = R.done() != 0u;
+      // not the lean step's case (never in the canonical loop), or the test hook: hand the env to
+      // k_env_fixup before its step t
+      if (!was_done && (!lean_ok(R, act) || t == s.redo_at)) {
         srng = srng0;
         duo_store_env_private<true>(s, i, R);
         rngs[i] = srng;
         park = (uint32_t)t | kParkRedo;
         live = false;
       } else {
-        const bool was_done = R.done() != 0u;
-        finish = !was_done && step_regs<true>(R, act, s, i, na PH_PASS);
+        stepped = !was_done;
+        finish = stepped && step_lean(R, act[0], na, turn_end);
         if (finish) R.set_done(1u);
         ended = was_done || finish;
         PH(0);
-        D.pl[ag][l] = pack_player(R.P);
-        D.cells[ag][l] = R.cells_a;
-        D.heads[ag][l] = mbits_u4(bits_of(R.sta));
-        if (na != ag) D.heads[na][l] = mbits_u4(bits_of(R.stn));
-#pragma unroll
-        for (int k = 0; k < 7; k++)
-          D.deckr[b3][k][l] = make_uint4(R.d[4 * k], R.d[4 * k + 1], R.d[4 * k + 2], R.d[4 * k + 3]);
+        D.pl[ag][l] = pack_player(R.P);                    // (the drawing wave's, at a turn end)
         PH(1);
       }
     }
@@ -3545,20 +3668,17 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, uint32_t *_
         const int na1 = (int)next_player((uint32_t)ag1, R.n_players());
         const MBits bs = bits_of(R.sel), ba = bits_of(R.sta), bn = bits_of(R.stn);
         const uint32_t info = (R.info_steps >> (8 * ag)) & 0xffu;
-        const uint32_t meta = kMetaValid | (R.moved ? kMetaMoved : 0u) | (uint32_t)ag << 2 | (uint32_t)na << 4 |
-                              (uint32_t)na1 << 6 | info << 8 | (ended ? kMetaEnded : 0u) | (uint32_t)ag1 << 24;
-        uint4(*ring)[64] = D.ring[t & 1];
-#pragma unroll
-        for (int k = 0; k < 3; k++) ring[k][l] = make_uint4(R.sh[4 * k], R.sh[4 * k + 1], R.sh[4 * k + 2], R.sh[4 * k + 3]);
-        ring[3][l] = make_uint4(bs.w0, bs.w1, bs.w2, meta);
-        ring[4][l] = make_uint4(ba.w0, ba.w1, ba.w2,
-                                (uint32_t)act[0] | (uint32_t)act[1] << 8 | (uint32_t)act[2] << 16 | (uint32_t)act[3] << 24);
-        ring[5][l] = make_uint4(bn.w0, bn.w1, bn.w2, (uint32_t)act[4]);
-        ring[6][l] = R.g2;
-        R.moved = false;
-        if (ag1 != ag) {                                   // turn change: ag1 == na acts next, its deck
-#pragma unroll                                             // as the storing wave last stored it
-          for (int k = 0; k < 7; k++) {
+        const uint32_t meta = kMetaValid | (uint32_t)ag << 2 | (uint32_t)na << 4 | (uint32_t)na1 << 6 | info << 8 |
+                              (ended ? kMetaEnded : 0u) | (stepped ? kMetaStepped : 0u) | (uint32_t)ag1 << 24;
+        uint4(*ring)[64] = D.ring[c3];
+        ring[0][l] = make_uint4(R.sh[0], R.sh[1], R.sh[2], R.sh[3]);
+        ring[1][l] = make_uint4(bs.w0, bs.w1, bs.w2, meta);
+        ring[2][l] = make_uint4(ba.w0, ba.w1, ba.w2, (uint32_t)act[0]);   // (lean: the other heads 0)
+        ring[3][l] = make_uint4(bn.w0, bn.w1, bn.w2, (R.P.n_active & 0xffu) << 8);
+        D.srng[c3][l] = srng;
+        if (ag1 != ag) {                                   // turn change: ag1 == na acts next, its hand
+#pragma unroll                                             // from the drawing wave's deck
+          for (int k = 1; k < 3; k++) {
             const uint4 v = D.img[ag1][k][l];
             R.d[4 * k] = v.x; R.d[4 * k + 1] = v.y; R.d[4 * k + 2] = v.z; R.d[4 * k + 3] = v.w;
           }
@@ -3566,7 +3686,10 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, uint32_t *_
           R.cells_a = R.cells_n;
           R.sta = R.stn;
           R.stn = heads_of(mbits_of(D.heads[na1][l]));
-          R.cells_n = D.cells[na1][l];
+          uint2 cn = cells[3];                             // (selects: no indexed registers)
+#pragma unroll
+          for (int p = 2; p >= 0; p--) cn = na1 == p ? cells[p] : cn;
+          R.cells_n = cn;
           R.na_active = (D.pl[na1][l].y >> 16) & 0xffu;
         }
         if (ended) {                                       // hand the env to k_env_fixup
@@ -3578,143 +3701,228 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, uint32_t *_
         ag = ag1;
         na = na1;
       } else {
-        D.ring[t & 1][3][l] = make_uint4(0u, 0u, 0u, 0u);  // no record
+        D.ring[c3][1][l] = make_uint4(0u, 0u, 0u, 0u);     // no record
       }
     }
     PH(3);
     __syncthreads();                                       // Y_t
     PH(4);
-    b3 = b3 == 2 ? 0 : b3 + 1;
+    c3 = mod3_next(c3);
   }
-  __syncthreads();                                         // X_{steps + 1}: every record stored
+  __syncthreads();                                         // X_{steps + 2}: every record stored
   PH_FLUSH(s_glob);
   if (live) {                                              // env-level private state back to HBM
-    R.flags |= D.sflags[l];                                // (the drawing wave's hazard flags)
+    R.flags |= D.sflags[l] | D.wflags[l];                  // (the other waves' hazard flags)
     duo_store_env_private<true>(s, i, R);
     rngs[i] = srng;
-  } else if (l < ne && D.sflags[l]) {                      // a parked env: flags of its last draws
-    reinterpret_cast<uint32_t *>(s.priv + i)[7] = R.flags | D.sflags[l];
+  } else if (l < ne && (D.sflags[l] | D.wflags[l])) {      // a parked env: flags of its last records
+    reinterpret_cast<uint32_t *>(s.priv + i)[7] = R.flags | D.sflags[l] | D.wflags[l];
   }
   if (l < ne) s.park[i] = park;
-  lds_store_wave<TrioLds, 64>(D, s, 0, ne);                // every player's records (cooperative)
+  trio_store_players(D, s, ne);                            // every player's records (cooperative)
 }
 
+// The drawing wave keeps every player's deck (img).  At odd t it takes records t - 1 and t: each
+// record's play replayed on the acting player's deck (the hand and active piles, as
+// Deck::activate does); then one pass over the turn ends of either record (discard + draws,
+// duo_turn_end: the env rng is this wave's).  Every granule a record changed goes to the storing
+// waves (deckr, dmask).
 DEV void trio_drawer(TrioLds &D, const DevState &s_glob, int steps) {
   const int l = (int)threadIdx.x - 64;
   const size_t wbase = (size_t)blockIdx.x * 64;
   const DevState s = wave_view(s_glob, wbase);
   const size_t i = (size_t)l;
   const bool live = wbase + (size_t)l < s_glob.n;
-  uint32_t rng = live ? reinterpret_cast<const uint32_t *>(s.priv + i)[0] : 0u;   // the env rng
+  uint32_t rng = 0u;                                       // the env rng
+  if (live) {
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+      const uint4 *src = reinterpret_cast<const uint4 *>(deck_ptr(s, i, p));
+#pragma unroll
+      for (int k = 0; k < 7; k++) D.img[p][k][l] = src[k];
+    }
+    rng = reinterpret_cast<const uint32_t *>(s.priv + i)[0];
+  }
   D.sflags[l] = 0u;
   __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();                                         // B
+  __syncthreads();                                         // B: the decks are in LDS
   PH_DECL;
-  int b3 = 0;
-  for (int t = 0; t <= steps; t++) {
+  int c3 = 0;                                              // t % 3
+  for (int t = 0; t <= steps + 1; t++) {
     __syncthreads();                                       // X_t
     __syncthreads();                                       // Y_t
     PH(8);
-    if (t < steps) {                                       // record t's turn ends
-      const uint32_t meta = D.ring[t & 1][3][l].w;
-      const int ag = (int)((meta >> 2) & 3u);
-      const bool te = live && (meta & kMetaValid) && (int)(meta >> 24) != ag;
-      if (__builtin_amdgcn_ballot_w64(te) && te) {
-        uint4 dk[7];
+    if ((t & 1) && t - 1 < steps) {                        // records t - 1 and t
+      const int slot[2] = {mod3_prev(c3), c3};
+      uint32_t dm[2] = {0u, 0u};
+      int agj[2] = {0, 0};
+      bool te[2] = {false, false};
 #pragma unroll
-        for (int k = 0; k < 7; k++) dk[k] = D.deckr[b3][k][l];
-        const uint4 x = D.ring[t & 1][4][l];
+      for (int j = 0; j < 2; j++) {                        // the plays, in record order
+        if (t - 1 + j >= steps) continue;                  // (uniform)
+        const uint32_t meta = D.ring[slot[j]][1][l].w;
+        const int ag = (int)((meta >> 2) & 3u);
+        const bool rec = live && (meta & kMetaValid) && (meta & kMetaStepped);
+        agj[j] = ag;
+        te[j] = rec && (int)(meta >> 24) != ag;
+        const int a_play = (int)(D.ring[slot[j]][2][l].w & 0xffu);
+        if (rec && a_play) {                               // Deck::activate (cards.cpp:242-253)
+          uint32_t d[28];
+          uint4 old[7];
+#pragma unroll
+          for (int k = 1; k < 4; k++) {                    // (hand and active piles: granules 1..3)
+            old[k] = D.img[ag][k][l];
+            d[4 * k] = old[k].x; d[4 * k + 1] = old[k].y; d[4 * k + 2] = old[k].z; d[4 * k + 3] = old[k].w;
+          }
+          pile_add<COG_DECK_HAND>(d, a_play - 1, 0xffu);
+          pile_add<COG_DECK_ACTIVE>(d, a_play - 1, 1u);
+#pragma unroll
+          for (int k = 1; k < 4; k++) {
+            const uint4 v = make_uint4(d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]);
+            if (ne4(v, old[k])) {
+              dm[j] |= 1u << k;
+              D.img[ag][k][l] = v;
+              D.deckr[slot[j]][k][l] = v;
+            }
+          }
+        }
+      }
+      const bool any = te[0] || te[1];                     // (at most one of them)
+      if (__builtin_amdgcn_ballot_w64(any) && any) {       // the turn end's discard + draws
+        const int j = te[1] ? 1 : 0, sl = te[1] ? slot[1] : slot[0], ag = te[1] ? agj[1] : agj[0];
+        uint4 dk[7], old[7];
+#pragma unroll
+        for (int k = 0; k < 7; k++) old[k] = dk[k] = D.img[ag][k][l];
+        const uint4 x = D.ring[sl][2][l];
         MBits ba{x.x, x.y, x.z};
         duo_turn_end(D, l, ag, dk, ba, rng);
+        D.ring[sl][2][l] = make_uint4(ba.w0, ba.w1, ba.w2, x.w);
+        uint32_t dd = 0;
 #pragma unroll
-        for (int k = 0; k < 7; k++) D.deckr[b3][k][l] = dk[k];
-        D.ring[t & 1][4][l] = make_uint4(ba.w0, ba.w1, ba.w2, x.w);
+        for (int k = 0; k < 7; k++)
+          if (ne4(dk[k], old[k])) {
+            dd |= 1u << k;
+            D.img[ag][k][l] = dk[k];
+            D.deckr[sl][k][l] = dk[k];
+          }
+        dm[0] |= j == 0 ? dd : 0u;
+        dm[1] |= j == 1 ? dd : 0u;
       }
+      D.dmask[slot[0]][l] = dm[0];
+      if (t < steps) D.dmask[slot[1]][l] = dm[1];
     }
     PH(9);
-    b3 = b3 == 2 ? 0 : b3 + 1;
+    c3 = mod3_next(c3);
   }
-  __syncthreads();                                         // X_{steps + 1}
+  __syncthreads();                                         // X_{steps + 2}
   if (live) reinterpret_cast<uint32_t *>(s.priv + i)[0] = rng;   // the env rng after its last draws
   PH_FLUSH(s_glob);
 }
 
-DEV void trio_storer(TrioLds &D, const DevState &s_glob, int steps, uint8_t *__restrict__ actions_glob) {
-  const int l = (int)threadIdx.x - 128;
+// The store phase of the trio on two waves, record t in [Y_{t+2}, X_{t+3}]: wave A (PART 0) the
+// ObsData shared block and the stored masks -- update_observation's heads of the acting player's
+// when the turn goes on (the lean step leaves them, step_lean) -- and wave B (PART 1) the decks,
+// the selected-mask record, the Info steps byte, the action, dones / agent_selection, and the
+// presampled draws (presample).  Each keeps its own images of what it stored last.
+template <int PART>
+DEV void trio_storer(TrioLds &D, const DevState &s_glob, int steps, const uint32_t *__restrict__ rngs_glob,
+                     uint8_t *__restrict__ actions_glob) {
+  const int l = (int)(threadIdx.x & 63);
   const size_t wbase = (size_t)blockIdx.x * 64;
   const DevState s = wave_view(s_glob, wbase);
   const size_t i = (size_t)l;
   const bool live = wbase + (size_t)l < s_glob.n;
   uint8_t *__restrict__ av = actions_glob + wbase * COG_ACTION_BYTES;
-  uint4 shb[3];
-  MBits selb = {0u, 0u, 0u}, stb[4];
-  uint32_t out = ~0u;                                      // dones[i] | agent_selection[i] << 8 as stored
+  uint4 shb0 = make_uint4(0u, 0u, 0u, 0u);                 // A: ObsData 16128.. as stored
+  MBits selb = {0u, 0u, 0u}, stb[4];                       // B: selected mask; A: stored masks
+  uint2 cells[4];                                          // A: every player's neighbourhood cache
+  uint32_t out = ~0u;                                      // B: dones[i] | agent_selection[i] << 8 as stored
+  RegEnv E;                                                // A: update_observation's inputs and flags
+  E.flags = 0u;
+  E.avail = 0u;
+  uint32_t x0 = 1u;                                        // B: the sampler state at step 0
   if (live) {
+    if (PART == 0) {
+      const uint4 *sh4 = reinterpret_cast<const uint4 *>(s.obs + i * COG_OBS_BYTES + COG_OBS_PHASE);
+      shb0 = sh4[0];
+      const uint4 sh1 = sh4[1], sh2 = sh4[2];
+      const uint4 *pv4 = reinterpret_cast<const uint4 *>(s.priv + i);
 #pragma unroll
-    for (int p = 0; p < 4; p++) {
-      const uint4 *dk = reinterpret_cast<const uint4 *>(deck_ptr(s, i, p));
-#pragma unroll
-      for (int k = 0; k < 7; k++) D.img[p][k][l] = dk[k];
+      for (int p = 0; p < 4; p++) {
+        stb[p] = mbits_of(s.heads[5 * i + 1 + p]);
+        cells[p] = reinterpret_cast<const uint2 *>(pv4 + 8)[p];
+      }
+      const uint4 g1 = pv4[1];
+      const uint32_t w[5] = {sh1.x, sh1.y, sh1.z, sh1.w, sh2.x};
+      E.avail = shop_avail_of(w, (g1.y >> 8) & 0xffu, g1.z);   // (no purchase in the lean step: fixed)
+    } else {
+      selb = mbits_of(s.heads[5 * i]);
+      x0 = rngs_glob[wbase + (size_t)l];
     }
-    const uint4 *sh4 = reinterpret_cast<const uint4 *>(s.obs + i * COG_OBS_BYTES + COG_OBS_PHASE);
-#pragma unroll
-    for (int k = 0; k < 3; k++) shb[k] = sh4[k];
-    selb = mbits_of(s.heads[5 * i]);
-#pragma unroll
-    for (int p = 0; p < 4; p++) stb[p] = mbits_of(s.heads[5 * i + 1 + p]);
+  }
+  if (PART == 1) {
+    D.pre[0][l] = presample(x0);                           // steps 0 and 1
+    D.pre[1][l] = presample(mr_jump(x0, kPow5));
   }
   __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();                                         // B: the image is in LDS
+  __syncthreads();                                         // B
   PH_DECL;
-  int b3 = 2;                                              // (t - 1) % 3
-  for (int t = 0; t <= steps; t++) {
+  int c3 = 1;                                              // (t - 2) % 3
+  for (int t = 0; t <= steps + 1; t++) {
     __syncthreads();                                       // X_t
     __syncthreads();                                       // Y_t
     PH(5);
-    if (t >= 1) {                                          // record t - 1
-      const int rb = (t - 1) & 1;
-      uint4 g[kRingG];
-#pragma unroll
-      for (int k = 0; k < kRingG; k++) g[k] = D.ring[rb][k][l];
-      const uint32_t meta = g[3].w;
+    if (PART == 1 && t < 2 && t + 2 < steps)               // steps 2 and 3 from the state at step 0
+      D.pre[t & 1][l] = presample(mr_jump(x0, t ? kPow15 : kPow10));
+    if (t >= 2) {                                          // record t - 2
+      const int sl = c3;
+      const uint4 m = D.ring[sl][1][l];
+      const uint32_t meta = m.w;
       const bool rec = live && (meta & kMetaValid);
       const int ag = (int)((meta >> 2) & 3u), na = (int)((meta >> 4) & 3u);
-      if (rec) {
-        uint4 dk[7];
-        uint32_t dm = 0;                                   // deck granules that changed
+      if (PART == 1 && rec && t + 2 < steps)               // step t + 2's draws: the state step t - 1
+        D.pre[t & 1][l] = presample(mr_jump(D.srng[sl][l], kPow15));   // starts at, + 15 draws
+      if (rec && PART == 0) {
+        const uint4 g0 = D.ring[sl][0][l], x = D.ring[sl][2][l];
+        MBits ba{x.x, x.y, x.z};
+        if ((int)(meta >> 24) == ag && (meta & kMetaStepped)) {   // the turn goes on: update_observation of
+          Heads h = heads_of(ba);                          // ag's stored mask (environment.cpp:252-279)
+          const uint32_t phase = g0.x & 0xffu;
+          const float r0 = __uint_as_float(g0.y), r1 = __uint_as_float(g0.z), r2 = __uint_as_float(g0.w);
+          const uint32_t n_active = (D.ring[sl][3][l].w >> 8) & 0xffu;
+          uint2 ca = cells[3];                             // (selects: no indexed registers)
 #pragma unroll
-        for (int k = 0; k < 7; k++) {
-          dk[k] = D.deckr[b3][k][l];
-          if (ne4(dk[k], D.img[ag][k][l])) dm |= 1u << k;
+          for (int p = 2; p >= 0; p--) ca = ag == p ? cells[p] : ca;
+          h.move = phase == COG_PHASE_MOVEMENT ? E.move_bits(ca, r0, r1, r2, n_active) : 1u;
+          h.shop = phase == COG_PHASE_BUYING ? E.shop_bits(r2) : 1u;
+          ba = bits_of(h);
         }
-#pragma unroll
-        for (int k = 0; k < 7; k++)
-          if ((dm >> k) & 1u) D.img[ag][k][l] = dk[k];
         PH(6);
         uint8_t *ob = s.obs + i * COG_OBS_BYTES;
-        s.info[i * COG_INFO_BYTES + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag] = (uint8_t)(meta >> 8);
-        if (meta & kMetaMoved) reinterpret_cast<uint4 *>(s.priv + i)[2] = g[6];
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-          if (ne4(g[k], shb[k])) reinterpret_cast<uint4 *>(ob + COG_OBS_PHASE)[k] = g[k];
-          shb[k] = g[k];
-        }
+        if (ne4(g0, shb0)) reinterpret_cast<uint4 *>(ob + COG_OBS_PHASE)[0] = g0;
+        shb0 = g0;
         uint8_t *deck = deck_ptr(s, i, ag);
-#pragma unroll
-        for (int k = 0; k < 7; k++)
-          if ((dm >> k) & 1u) reinterpret_cast<uint4 *>(deck)[k] = dk[k];
-        const MBits bs{g[3].x, g[3].y, g[3].z}, ba{g[4].x, g[4].y, g[4].z};
-        store_mask_record(reinterpret_cast<uint4 *>(s.sel + i * COG_MASK_BYTES), bs, mask_diff_granules(bs, selb));
-        selb = bs;
         store_mask_record(reinterpret_cast<uint4 *>(deck + COG_PD_MASK), ba, mask_diff_granules(ba, selm(stb, ag)));
         setm(stb, ag, ba);
         if (na != ag) {
-          const MBits bn{g[5].x, g[5].y, g[5].z};
+          const uint4 y = D.ring[sl][3][l];
+          const MBits bn{y.x, y.y, y.z};
           store_mask_record(reinterpret_cast<uint4 *>(deck_ptr(s, i, na) + COG_PD_MASK), bn,
                             mask_diff_granules(bn, selm(stb, na)));
           setm(stb, na, bn);
         }
-        reinterpret_cast<uint2 *>(av + i * COG_ACTION_BYTES)[0] = make_uint2(g[4].w, g[5].w);
+      }
+      if (rec && PART == 1) {
+        const uint32_t dm = D.dmask[sl][l];                // deck granules that changed (drawing wave)
+        uint8_t *deck = deck_ptr(s, i, ag);
+#pragma unroll
+        for (int k = 0; k < 7; k++)
+          if ((dm >> k) & 1u) reinterpret_cast<uint4 *>(deck)[k] = D.deckr[sl][k][l];
+        s.info[i * COG_INFO_BYTES + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag] = (uint8_t)(meta >> 8);
+        const MBits bs{m.x, m.y, m.z};
+        store_mask_record(reinterpret_cast<uint4 *>(s.sel + i * COG_MASK_BYTES), bs, mask_diff_granules(bs, selb));
+        selb = bs;
+        reinterpret_cast<uint2 *>(av + i * COG_ACTION_BYTES)[0] = make_uint2(D.ring[sl][2][l].w, 0u);   // (lean: heads 1-4 are 0)
         if (!(meta & kMetaEnded)) {                        // dones[i] = 0, agent_selection[i]
           const uint32_t agent = meta >> 24;               // (an ended episode: k_env_fixup)
           if (out & 0xffu) s.done[i] = 0;
@@ -3724,14 +3932,24 @@ DEV void trio_storer(TrioLds &D, const DevState &s_glob, int steps, uint8_t *__r
       }
     }
     PH(13);
-    b3 = b3 == 2 ? 0 : b3 + 1;
+    c3 = mod3_next(c3);
   }
-  __syncthreads();                                         // X_{steps + 1}
+  // A: the stored-mask bit vectors as stored (the epilogue's; the drawing wave's turn ends
+  // included), and its hazard flags (update_observation's lookups) for the stepping wave to merge
+  if (PART == 0) {
+    if (live) {
+#pragma unroll
+      for (int p = 0; p < 4; p++) D.heads[p][l] = mbits_u4(stb[p]);
+    }
+    D.wflags[l] = E.flags;
+  }
+  __syncthreads();                                         // X_{steps + 2}
   PH_FLUSH(s_glob);
 }
 
+// four waves per workgroup: stepping, drawing and two storing waves
 template <int SRC>
-__global__ void __launch_bounds__(192) k_env_rollout_trio(DevState s, int steps, uint32_t *__restrict__ rngs,
+__global__ void __launch_bounds__(256) k_env_rollout_trio(DevState s, int steps, uint32_t *__restrict__ rngs,
                                                           uint8_t *__restrict__ actions_out) {
   __shared__ TrioLds D;
   const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform
@@ -3741,8 +3959,10 @@ __global__ void __launch_bounds__(192) k_env_rollout_trio(DevState s, int steps,
     trio_stepper<SRC>(D, s, steps, rngs);
   } else if (role == 1) {
     trio_drawer(D, s, steps);
+  } else if (role == 2) {
+    trio_storer<0>(D, s, steps, rngs, actions_out);
   } else {
-    trio_storer(D, s, steps, actions_out);
+    trio_storer<1>(D, s, steps, rngs, actions_out);
   }
 }
 
@@ -4075,7 +4295,7 @@ int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rn
       hipLaunchKernelGGL((k_env_rollout_duo<MASK_STORED>), g, dim3(128), 0, st, sd, steps, d_rng, d_actions);
       hipLaunchKernelGGL((k_env_fixup<MASK_STORED>), g, dim3(64), 0, st, sd, steps, d_rng, d_actions);
     } else if (kind == RK_TRIO) {                          // selected masks, >= 3 players
-      hipLaunchKernelGGL((k_env_rollout_trio<MASK_SELECTED>), g, dim3(192), 0, st, sd, steps, d_rng, d_actions);
+      hipLaunchKernelGGL((k_env_rollout_trio<MASK_SELECTED>), g, dim3(256), 0, st, sd, steps, d_rng, d_actions);
       hipLaunchKernelGGL((k_env_fixup<MASK_SELECTED>), g, dim3(64), 0, st, sd, steps, d_rng, d_actions);
     } else {
       hipLaunchKernelGGL((k_env_rollout_duo<MASK_SELECTED>), g, dim3(128), 0, st, sd, steps, d_rng, d_actions);

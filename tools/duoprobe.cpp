@@ -51,13 +51,18 @@ int main(int argc, char **argv) {
     const double r1000 = timed(1000, 5), r20 = timed(20, 25);
     printf("%s n=%6zu  %6.3f us/step (1000-step launches)  20-step launch %7.2f us (%5.3f us/step)\n", tag, n,
            r1000 / 1000, r20, r20 / 20);
+    if (getenv("PROBE_SHORT")) {                           // the fixed cost: 1-, 2- and 5-step launches
+      const double r1 = timed(1, 25), r2 = timed(2, 25), r5 = timed(5, 25);
+      printf("%s n=%6zu  launch of 1 / 2 / 5 steps: %7.2f %7.2f %7.2f us  (fixed ~ %.2f us)\n", tag, n, r1, r2, r5,
+             r1 - (r5 - r1) / 4);
+    }
     fflush(stdout);
 #ifdef COG_STAMPS
     {
-      // the duo: 2 waves per workgroup (stepping, storing); the trio ($COG_TRIO unset): 3 (stepping,
-      // drawing, storing).  Each wave's PH slots (cog_engine.hip): its own phase names below.
+      // the duo: 2 waves per workgroup (stepping, storing); the trio ($COG_TRIO unset): 4 (stepping,
+      // drawing, storing A, storing B).  Each wave's PH slots (cog_engine.hip): its phase names below.
       const char *trio_env = getenv("COG_TRIO");
-      const int wpg = (trio_env && *trio_env == '0') ? 2 : 3;
+      const int wpg = (trio_env && *trio_env == '0') ? 2 : 4;
       const size_t waves = (size_t)wpg * ((n + 63) / 64);
       constexpr int K = 16;
       unsigned long long *d;
@@ -78,9 +83,9 @@ int main(int argc, char **argv) {
                                      "", "", "stores", "", ""};
       const char *draw_names[16] = {"", "", "", "", "", "", "", "", "wait X, Y", "turn-end draws", "", "", "", "", "",
                                     ""};
-      const char *role_name[3] = {"stepping", wpg == 3 ? "drawing" : "storing", "storing"};
+      const char *role_name[4] = {"stepping", wpg == 4 ? "drawing" : "storing", "storing A", "storing B"};
       for (int role = 0; role < wpg; role++) {
-        const char **pn = role == 0 ? step_names : (wpg == 3 && role == 1) ? draw_names : store_names;
+        const char **pn = role == 0 ? step_names : (wpg == 4 && role == 1) ? draw_names : store_names;
         double tot = 0;
         printf("  %s wave:\n", role_name[role]);
         for (int k = 0; k < 16; k++) {
