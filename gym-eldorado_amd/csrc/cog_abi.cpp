@@ -333,8 +333,33 @@ namespace {
 
 bool single(const cog_env *e) { return e->sh.size() == 1; }
 
+// Envs with host views, for cog_sampler_sample: when the masks it gets are one env shard's own
+// pinned selected-mask view on the sampler shard's device, and that shard's views equal HBM
+// (host_synced: its last call published and completed), the sampler reads the same records in
+// HBM instead of over PCIe.  The views are the env's outputs -- the engine
+// never reads them back, its step included -- so a caller's writes into them go unseen either way.
+std::mutex g_host_envs_mu;
+std::vector<cog_env *> g_host_envs;
+
+void host_env_register(cog_env *e, bool on) {
+  std::lock_guard<std::mutex> lk(g_host_envs_mu);
+  auto it = std::find(g_host_envs.begin(), g_host_envs.end(), e);
+  if (on && it == g_host_envs.end()) g_host_envs.push_back(e);
+  if (!on && it != g_host_envs.end()) g_host_envs.erase(it);
+}
+
+const uint8_t *env_masks_in_hbm(const cog_action_mask_t *masks, size_t n, int device) {
+  if (std::getenv("COG_NO_HBM_MASKS")) return nullptr;    // (A/B)
+  std::lock_guard<std::mutex> lk(g_host_envs_mu);
+  for (cog_env *e : g_host_envs)
+    for (const EnvShard &k : e->sh)
+      if (e->h_sel + k.first == masks && k.n == n && k.device == device && k.host_synced) return k.s.sel;
+  return nullptr;
+}
+
 void env_free(cog_env *e) {
   if (!e) return;
+  host_env_register(e, false);
   for (EnvShard &k : e->sh) {
     DeviceGuard g(k.device);
     if (k.stream) (void)hipStreamSynchronize(k.stream);
@@ -381,6 +406,8 @@ int sync_fast(cog_env *e) {
 
 int status_to_rc(uint32_t flags, uint32_t errors) {
   if (errors) {
+    if (flags & cog::F_SYNC_TIMEOUT)
+      return fail(COG_ERR_HIP, "internal error: a rollout wave's progress wait timed out (outputs invalid)");
     if (flags & cog::F_GRID_OVER)
       return fail(COG_ERR_MAPGEN, "map generation produced a map larger than the 48x48 observation grid");
     return fail(COG_ERR_MAPGEN, "Failed to generate map in specified maximum number of attempts");
@@ -828,6 +855,7 @@ static int alloc_host_views(cog_env *env) {
     k.mir_valid = false;
   }
   env->host = true;
+  host_env_register(env, true);
   return refresh_full(env);
 }
 
@@ -1131,10 +1159,13 @@ int cog_sampler_sample(cog_sampler *s, const cog_action_mask_t *masks, size_t n)
   for (SamplerShard &k : s->sh) {
     if (!k.n) continue;
     DeviceGuard g(k.device);
-    const uint8_t *dm = zc_device(masks + k.first, k.n * COG_MASK_BYTES);   // read in place when pinned
-    if (!dm || !zc_same_on(k.device, masks + k.first)) {
-      HIPCHK(hipMemcpyAsync(k.d_masks, masks + k.first, k.n * COG_MASK_BYTES, hipMemcpyHostToDevice, k.stream));
-      dm = k.d_masks;
+    const uint8_t *dm = env_masks_in_hbm(masks + k.first, k.n, k.device);   // an env's own view: HBM
+    if (!dm) {
+      dm = zc_device(masks + k.first, k.n * COG_MASK_BYTES);                // else read in place when pinned
+      if (!dm || !zc_same_on(k.device, masks + k.first)) {
+        HIPCHK(hipMemcpyAsync(k.d_masks, masks + k.first, k.n * COG_MASK_BYTES, hipMemcpyHostToDevice, k.stream));
+        dm = k.d_masks;
+      }
     }
     int rc = sampler_run(k, s->h_actions, dm, k.stream, true, true);
     if (rc || (rc = signal_enqueue(k.done, k.stream))) return rc;

@@ -43,6 +43,7 @@ constexpr uint32_t F_OOB_LOOKUP = 0x20u;
 constexpr uint32_t F_SCAN_OVER = 0x40u;
 constexpr uint32_t F_B_START_LT4 = 0x80u;
 constexpr uint32_t F_BAD_ACTION = 0x100u;
+constexpr uint32_t F_SYNC_TIMEOUT = 0x200u;  // (device status only) a trio wave's progress wait timed out
 constexpr uint32_t F_ERROR_MASK = F_MAPGEN_FAIL | F_GRID_OVER;
 
 struct PlayerPriv {                  // Player + Deck private members (player.h:60-75, cards.h:137-145)
@@ -161,7 +162,8 @@ int launch_sample_step(const DevState &s, int mask_source, uint32_t *d_rng, uint
 // rollout's deferred turn end may run on shards of <= 16,384 envs with the selected masks)
 int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions,
                    void *stream, bool defer_ok = false);
-int rollout_kind_of(size_t n, int mask_source, bool defer_ok);   // 0 duo, 1 wave, 2 pipe, 3 trio (launch_rollout)
+int rollout_kind_of(size_t n, int mask_source, bool defer_ok);
+int trio_epw(size_t n);                                          // envs per trio workgroup (32 or 64)   // 0 duo, 1 wave, 2 pipe, 3 trio (launch_rollout)
 int launch_seed_sampler(size_t n, uint64_t seed, size_t first, uint32_t *d_rng, void *stream);
 // completion word: stores seq into *d_word (device address of a pinned host word) once every
 // earlier packet of the stream has completed

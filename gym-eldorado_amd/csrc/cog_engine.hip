@@ -1446,7 +1446,7 @@ DEV void sample_heads(const Heads &h, uint32_t &rng, uint8_t out[5], const UidEn
 // state is the one they start from and every head is non-empty -- else, or when a head other than
 // head 0 holds two or more candidates, it draws the sequential way (sample_heads).  The values
 // are the same either way (cog_rng.h jump-ahead: x * 16807^j mod (2^31 - 1)).
-constexpr uint32_t kPow5 = mr_pow(5), kPow10 = mr_pow(10), kPow15 = mr_pow(15);
+constexpr uint32_t kPow15 = mr_pow(15);
 DEV uint4 presample(uint32_t x) {                          // x: the state the step starts from
   uint32_t y = x, r0 = 0, risk = 0;
 #pragma unroll
@@ -3389,7 +3389,7 @@ DEV void setm(MBits b[4], int p, const MBits &v) {
 // mask gains the drawn cards; the player's counters and stored-mask bits go back to the LDS
 // records the stepping wave reads when ag acts again.
 template <class Lds>
-DEV void duo_turn_end(Lds &D, int l, int ag, uint4 dk[7], MBits &ba, uint32_t &rng) {
+DEV void duo_turn_end(Lds &D, int l, int ag, uint4 dk[7], MBits &ba, uint32_t &rng, uint32_t &flags) {
   RegEnv E;
 #pragma unroll
   for (int k = 0; k < 7; k++) {
@@ -3407,7 +3407,7 @@ DEV void duo_turn_end(Lds &D, int l, int ag, uint4 dk[7], MBits &ba, uint32_t &r
   rng = E.rng;
   D.pl[ag][l] = pack_player(E.P);
   D.heads[ag][l] = mbits_u4(ba);
-  if (E.flags) D.sflags[l] |= E.flags;
+  flags |= E.flags;
 }
 
 DEV void duo_storer(DuoLds &D, const DevState &s_glob, int steps, uint8_t *__restrict__ actions_glob) {
@@ -3529,44 +3529,99 @@ __global__ void __launch_bounds__(128) k_env_rollout_duo(DevState s, int steps, 
 // presampled draws (presample).  History (8,192 envs, device us per step in 1,000-step launches,
 // profiles/r04*_trio*.txt): the duo 2.45; its storing wave doing the draws 3.17 (it set the pace,
 // profiles/r04d_duo_defer.txt); the draws on a third wave 1.96; lean step, hand-only stepping
-// wave, presampled draws and two storing waves 1.80; turn ends batched over two records (below).
+// wave, presampled draws and two storing waves, in barrier lockstep 1.80 (the drawing wave's turn
+// ends set the pace); turn ends batched over two records, still in lockstep, 1.86 (a two-record
+// round is as long as the two it replaces); decoupled through progress counters (below).
 //
-// Pipeline, per step t (barriers X_t, Y_t; every wave executes every barrier):
-//   stepping wave  [Y_{t-1}, X_t] step t;  [X_t, Y_t] record t -> ring[t % 3], turn change
-//   drawing wave   at odd t, [Y_t, X_{t+1}]: records t - 1 and t -- the plays replayed on the
-//                  acting players' decks (img), then ONE turn-end pass: a lean turn lasts at least
-//                  two steps (pass in MOVEMENT, pass in BUYING), so a player ends at most one turn
-//                  in two records, and the pass runs once per two steps
-//   storing waves  [Y_{t+2}, X_{t+3}] record t (ring, deckr / dmask from the drawing wave)
-// The loop runs steps + 2 rounds (the last two drain the pipeline), then one more barrier.  Why
-// the stepping wave's reads are safe: it reads a player's hand (img), counters (pl) or stored mask
-// (heads) only when that player becomes the agent or the one after it, and with >= 3 players and
-// turns of >= 2 steps, that player's last turn end lies >= 2 steps back: the drawing wave finished
-// it by then (X_{t_e + 2}).
+// The waves run as a pipeline over LDS buffers, synchronised by progress counters in LDS (cnt[],
+// release / acquire at workgroup scope; a waiting wave sleeps between polls) instead of barriers,
+// so each runs at its own average rate:
+//   stepping wave  step t: ring slot t % 8 free (record t - 8 stored by both storing waves), step
+//                  t's presampled draws written (cnt[PRE] > t - 4); step; record t -> ring,
+//                  cnt[REC] = t + 1; at a turn change, the drawing wave past the last turn ends of
+//                  the new agent (its hand, counters) and of the player after it (its stored mask,
+//                  n_active) -- per player, the step its last turn ended (tend[]); with >= 3
+//                  players and turns of >= 2 steps those lie >= 2 steps back.
+//   drawing wave   records r, r + 1 (r even) once written: the plays replayed on the acting players'
+//                  decks (img: two byte updates each), then ONE turn-end pass -- a lean turn lasts at least two steps (pass
+//                  in MOVEMENT, pass in BUYING), so a player ends at most one turn in two records --
+//                  and the deck granules each record changed (ring granule 3, bits 16..22);
+//                  cnt[DRAW] = r + 2
+//   storing wave B record r once written: step r + 4's presampled draws (cnt[PRE] = r + 1), the
+//                  selected mask, Info, action, dones / agent_selection; on a second cursor
+//                  kTrioBLag records behind, once drawn, the changed deck granules straight from img -- a granule a later record changed again may
+//                  already hold that later value (or be read mid-update), but that record stores
+//                  it again, in order, so the last store of every granule is its final value;
+//                  cnt[STB] = r + 1
+//   storing wave A record r once drawn: ObsData, the stored masks; cnt[STA] = r + 1
+// The waits form no cycle: every wait of the stepping wave needs only records it has published.
+// A wait that outlasts kTrioSpinLimit polls (a bug, never a slow wave) sets F_SYNC_TIMEOUT and the
+// host error word and goes on, so that no fault can hang the GPU.
 //
 // record t: 0 ObsData 16128.. (phase, resources; the lean step never changes the shop), 1 selected-
 // mask bits + meta, 2 the acting player's stored-mask bits (saved mask at a turn end: the drawing
 // wave adds the drawn cards) + action byte 0, 3 the next player's stored-mask bits + n_active of
-// the acting player << 8.  The neighbourhood caches never change in the lean step (no moves): the
-// stepping wave and storing wave A keep their own copies, and the epilogue does not store them.
+// the acting player << 8 + the deck granules the record changed << 16 (drawing wave).  The
+// neighbourhood caches never change in the lean step (no moves): the stepping wave and storing wave
+// A keep their own copies, and the epilogue does not store them.
 constexpr int kTrioRingG = 4;
+constexpr int kTrioDepth = 8;                              // ring slots (records in flight)
+constexpr int kTrioLead = 4;                               // presampled draws: steps ahead of the record
+constexpr int kTrioBLag = 2;                               // storing wave B: deck cursor behind its front
+enum TrioCnt : int { CNT_REC = 0, CNT_DRAW, CNT_STA, CNT_STB, CNT_PRE, CNT_FIN, kTrioCnts };
+constexpr uint32_t kTrioSpinLimit = 1u << 21;             // polls (~0.2 s)
 struct TrioLds {
   uint4 img[4][7][64];                // every player's DeckObs (the drawing wave's)
-  uint4 deckr[3][7][64];              // record t's DeckObs granules that changed, t % 3
-  uint32_t dmask[3][64];              // ... which ones
-  uint4 ring[3][kTrioRingG][64];      // record t (above), t % 3
-  uint32_t srng[3][64];               // the sampler state after step t, t % 3
-  uint4 pre[2][64];                   // presampled draws of step t (storing wave B), t & 1
+  uint4 ring[kTrioDepth][kTrioRingG][64];   // record t (above), t % 8
+  uint32_t srng[kTrioDepth][64];      // the sampler state after step t, t % 8
+  uint3 pre[kTrioLead][64];           // step t's presampled draws, t % 4: state, head 0's draw | risk << 31, state after
   uint4 pl[4][64];
   uint4 heads[4][64];
-  uint32_t sflags[64];                // hazard flags of the drawing wave's draws
-  uint32_t wflags[64];                // ... and of storing wave A's update_observation
+  uint32_t flg[64];                   // the other waves' hazard flags (the stepping wave's epilogue)
+  uint32_t cnt[kTrioCnts];            // progress counters
   UidEntry tab[kUidTab];
 };
 static_assert(sizeof(TrioLds) <= 75520, "two trio workgroups per CU (measured: 78,336 B admit one)");
 
-DEV int mod3_next(int c) { return c == 2 ? 0 : c + 1; }
-DEV int mod3_prev(int c) { return c == 0 ? 2 : c - 1; }
+// A wave keeps the counters it last read (wave-uniform, in SGPRs) and reads them again -- all six
+// in one round trip -- only when the one it needs is short: the counters only grow, and what an
+// acquire read once made visible stays so.  A waiting wave sleeps between reads.
+struct TrioCnt6 {
+  uint32_t rec = 0, draw = 0, sta = 0, stb = 0, pre = 0, fin = 0;
+};
+DEV void cnt_read(const TrioLds &D, TrioCnt6 &c) {
+  uint32_t v[kTrioCnts];
+#pragma unroll
+  for (int k = 0; k < kTrioCnts; k++) v[k] = __hip_atomic_load(&D.cnt[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  c.rec = __builtin_amdgcn_readfirstlane(v[CNT_REC]);
+  c.draw = __builtin_amdgcn_readfirstlane(v[CNT_DRAW]);
+  c.sta = __builtin_amdgcn_readfirstlane(v[CNT_STA]);
+  c.stb = __builtin_amdgcn_readfirstlane(v[CNT_STB]);
+  c.pre = __builtin_amdgcn_readfirstlane(v[CNT_PRE]);
+  c.fin = __builtin_amdgcn_readfirstlane(v[CNT_FIN]);
+}
+DEV void cnt_store(TrioLds &D, int k, uint32_t v) {        // publishes this wave's earlier LDS writes
+  if ((threadIdx.x & 63) == 0) __hip_atomic_store(&D.cnt[k], v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// wait (wave-uniform) until counter `field` of c (a member of c) >= v
+DEV void cnt_wait(const TrioLds &D, TrioCnt6 &c, const uint32_t &field, uint32_t v, const DevState &s) {
+  if (field >= v) return;
+  for (uint32_t spins = 0;; spins++) {
+    cnt_read(D, c);
+    if (field >= v) return;
+    if (spins >= kTrioSpinLimit) {
+      if ((threadIdx.x & 63) == 0) {
+        atomicOr(&s.status[0], F_SYNC_TIMEOUT);
+        atomicAdd(&s.status[1], 1u);
+        *s.err = 1u;
+      }
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+DEV uint3 pre_pack(const uint4 p) { return make_uint3(p.x, p.y | p.w << 31, p.z); }
 
 // the epilogue's player records (lds_store_wave without the neighbourhood caches)
 DEV void trio_store_players(const TrioLds &D, const DevState &s, int ne) {
@@ -3580,17 +3635,18 @@ DEV void trio_store_players(const TrioLds &D, const DevState &s, int ne) {
 }
 
 template <int SRC>
-DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, uint32_t *__restrict__ rngs_glob) {
+DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, uint32_t *__restrict__ rngs_glob) {
   const int l = threadIdx.x;
-  const size_t wbase = (size_t)blockIdx.x * 64;
+  const size_t wbase = (size_t)blockIdx.x * epw;
   const DevState s = wave_view(s_glob, wbase);
   const size_t i = (size_t)l;
-  const int ne = (int)min((size_t)64, s_glob.n - wbase);
+  const int ne = (int)min((size_t)epw, s_glob.n - wbase);
   uint32_t *__restrict__ rngs = rngs_glob + wbase;
   bool live = l < ne;
   uint32_t park = kParkNone, srng = 0;
   RegEnv R;
   uint2 cells[4];                                          // every player's neighbourhood cache
+  int tend[4] = {-1, -1, -1, -1};                          // per player: the step its last turn ended
   int ag = 0, na = 0;
   if (live) {
     Snap S;
@@ -3621,7 +3677,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, uint32_t *_
   }
   R.tab = D.tab;
   __builtin_amdgcn_s_waitcnt(0);                           // (no per-iteration vmcnt wait covers them)
-  __syncthreads();                                         // B: the drawing wave loaded every deck
+  __syncthreads();                                         // B: every wave's prologue is done
 #pragma unroll
   for (int k = 0; k < 28; k++) R.d[k] = 0u;                // (only the hand pile is the stepping wave's:
   if (live) {                                              // bytes 21..41, granules 1 and 2)
@@ -3632,13 +3688,22 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, uint32_t *_
     }
   }
   PH_DECL;
-  int c3 = 0;                                              // t % 3
-  for (int t = 0; t <= steps + 1; t++) {
+  TrioCnt6 cc;
+  for (int t = 0; t < steps; t++) {
+    const int sl = t & (kTrioDepth - 1);
+    if (t >= kTrioDepth) {                                 // slot t % 8 free
+      cnt_wait(D, cc, cc.sta, (uint32_t)(t - kTrioDepth + 1), s_glob);
+      cnt_wait(D, cc, cc.stb, (uint32_t)(t - kTrioDepth + 1), s_glob);
+    }
+    if (t >= kTrioLead) cnt_wait(D, cc, cc.pre, (uint32_t)(t - kTrioLead + 1), s_glob);
+    PH(2);
     bool ended = false, finish = false, turn_end = false, stepped = false;
     uint8_t act[5];
-    if (t < steps && live) {
+    if (live) {
       const uint32_t srng0 = srng;
-      const bool fast = sample_presampled(R.sel, D.pre[t & 1][l], srng, act, R.tab);
+      const uint3 pr = D.pre[t & (kTrioLead - 1)][l];
+      const bool fast =
+          sample_presampled(R.sel, make_uint4(pr.x, pr.y & 0x7fffffffu, pr.z, pr.y >> 31), srng, act, R.tab);
       if (__builtin_amdgcn_ballot_w64(!fast) && !fast)     // (wave-uniform skip)
         step_action<SRC>(R, make_uint2(0u, 0u), srng, act);
       const bool was_done = R.done() != 0u;
@@ -3657,82 +3722,97 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, uint32_t *_
         ended = was_done || finish;
         PH(0);
         D.pl[ag][l] = pack_player(R.P);                    // (the drawing wave's, at a turn end)
-        PH(1);
       }
     }
-    __syncthreads();                                       // X_t
-    PH(2);
-    if (t < steps) {
-      if (live) {
-        const int ag1 = (int)R.agent();
-        const int na1 = (int)next_player((uint32_t)ag1, R.n_players());
-        const MBits bs = bits_of(R.sel), ba = bits_of(R.sta), bn = bits_of(R.stn);
-        const uint32_t info = (R.info_steps >> (8 * ag)) & 0xffu;
-        const uint32_t meta = kMetaValid | (uint32_t)ag << 2 | (uint32_t)na << 4 | (uint32_t)na1 << 6 | info << 8 |
-                              (ended ? kMetaEnded : 0u) | (stepped ? kMetaStepped : 0u) | (uint32_t)ag1 << 24;
-        uint4(*ring)[64] = D.ring[c3];
-        ring[0][l] = make_uint4(R.sh[0], R.sh[1], R.sh[2], R.sh[3]);
-        ring[1][l] = make_uint4(bs.w0, bs.w1, bs.w2, meta);
-        ring[2][l] = make_uint4(ba.w0, ba.w1, ba.w2, (uint32_t)act[0]);   // (lean: the other heads 0)
-        ring[3][l] = make_uint4(bn.w0, bn.w1, bn.w2, (R.P.n_active & 0xffu) << 8);
-        D.srng[c3][l] = srng;
-        if (ag1 != ag) {                                   // turn change: ag1 == na acts next, its hand
-#pragma unroll                                             // from the drawing wave's deck
-          for (int k = 1; k < 3; k++) {
-            const uint4 v = D.img[ag1][k][l];
-            R.d[4 * k] = v.x; R.d[4 * k + 1] = v.y; R.d[4 * k + 2] = v.z; R.d[4 * k + 3] = v.w;
-          }
-          R.P = unpack_player(D.pl[ag1][l]);
-          R.cells_a = R.cells_n;
-          R.sta = R.stn;
-          R.stn = heads_of(mbits_of(D.heads[na1][l]));
-          uint2 cn = cells[3];                             // (selects: no indexed registers)
+    uint4(*ring)[64] = D.ring[sl];
+    int ag1 = ag, na1 = na;
+    if (live) {
+      ag1 = (int)R.agent();
+      na1 = (int)next_player((uint32_t)ag1, R.n_players());
+      const MBits bs = bits_of(R.sel), ba = bits_of(R.sta), bn = bits_of(R.stn);
+      const uint32_t info = (R.info_steps >> (8 * ag)) & 0xffu;
+      const uint32_t meta = kMetaValid | (uint32_t)ag << 2 | (uint32_t)na << 4 | (uint32_t)na1 << 6 | info << 8 |
+                            (ended ? kMetaEnded : 0u) | (stepped ? kMetaStepped : 0u) | (uint32_t)ag1 << 24;
+      ring[0][l] = make_uint4(R.sh[0], R.sh[1], R.sh[2], R.sh[3]);
+      ring[1][l] = make_uint4(bs.w0, bs.w1, bs.w2, meta);
+      ring[2][l] = make_uint4(ba.w0, ba.w1, ba.w2, (uint32_t)act[0]);   // (lean: the other heads 0)
+      ring[3][l] = make_uint4(bn.w0, bn.w1, bn.w2, (R.P.n_active & 0xffu) << 8);
+      D.srng[sl][l] = srng;
+    } else {
+      ring[1][l] = make_uint4(0u, 0u, 0u, 0u);             // no record
+    }
+    cnt_store(D, CNT_REC, (uint32_t)(t + 1));
+    PH(1);
+    const bool tc = live && ag1 != ag;                     // turn change: ag1 == na acts next
+    if (__builtin_amdgcn_ballot_w64(tc)) {
+      int need = -1;                                       // the later of ag1's and na1's last turn ends
 #pragma unroll
-          for (int p = 2; p >= 0; p--) cn = na1 == p ? cells[p] : cn;
-          R.cells_n = cn;
-          R.na_active = (D.pl[na1][l].y >> 16) & 0xffu;
+      for (int p = 0; p < 4; p++) need = (p == ag1 || p == na1) ? max(need, tend[p]) : need;
+      // the drawing wave past record max(need) over the wave: its distance from t by ballots (no
+      // cross-lane shuffles, which go through LDS); >= 2 in play (>= 3 players, turns of >= 2
+      // steps), and from 5 on it asks for a little more than it needs
+      const bool w = tc && need >= 0;
+      if (__builtin_amdgcn_ballot_w64(w)) {
+        int dmin = 5;
+#pragma unroll
+        for (int d = 4; d >= 1; d--) dmin = __builtin_amdgcn_ballot_w64(w && need >= t - d) ? d : dmin;
+        cnt_wait(D, cc, cc.draw, (uint32_t)(t - dmin + 1), s_glob);
+      }
+      if (tc) {
+#pragma unroll
+        for (int p = 0; p < 4; p++) tend[p] = p == ag ? t : tend[p];
+#pragma unroll                                             // its hand from the drawing wave's deck
+        for (int k = 1; k < 3; k++) {
+          const uint4 v = D.img[ag1][k][l];
+          R.d[4 * k] = v.x; R.d[4 * k + 1] = v.y; R.d[4 * k + 2] = v.z; R.d[4 * k + 3] = v.w;
         }
-        if (ended) {                                       // hand the env to k_env_fixup
-          duo_store_env_private<true>(s, i, R);
-          rngs[i] = srng;
-          park = (uint32_t)t | (finish ? kParkFinish : 0u);
-          live = false;
-        }
-        ag = ag1;
-        na = na1;
-      } else {
-        D.ring[c3][1][l] = make_uint4(0u, 0u, 0u, 0u);     // no record
+        R.P = unpack_player(D.pl[ag1][l]);
+        R.cells_a = R.cells_n;
+        R.sta = R.stn;
+        R.stn = heads_of(mbits_of(D.heads[na1][l]));
+        uint2 cn = cells[3];                               // (selects: no indexed registers)
+#pragma unroll
+        for (int p = 2; p >= 0; p--) cn = na1 == p ? cells[p] : cn;
+        R.cells_n = cn;
+        R.na_active = (D.pl[na1][l].y >> 16) & 0xffu;
       }
     }
+    if (live && ended) {                                   // hand the env to k_env_fixup
+      duo_store_env_private<true>(s, i, R);
+      rngs[i] = srng;
+      park = (uint32_t)t | (finish ? kParkFinish : 0u);
+      live = false;
+    }
+    ag = ag1;
+    na = na1;
     PH(3);
-    __syncthreads();                                       // Y_t
-    PH(4);
-    c3 = mod3_next(c3);
   }
-  __syncthreads();                                         // X_{steps + 2}: every record stored
+  cnt_store(D, CNT_REC, (uint32_t)steps + 1u);             // the loop is over (storing wave A's epilogue)
+  cnt_wait(D, cc, cc.fin, 3u, s_glob);                        // the other waves are done
   PH_FLUSH(s_glob);
+  const uint32_t fl = D.flg[l];                            // their hazard flags
   if (live) {                                              // env-level private state back to HBM
-    R.flags |= D.sflags[l] | D.wflags[l];                  // (the other waves' hazard flags)
+    R.flags |= fl;
     duo_store_env_private<true>(s, i, R);
     rngs[i] = srng;
-  } else if (l < ne && (D.sflags[l] | D.wflags[l])) {      // a parked env: flags of its last records
-    reinterpret_cast<uint32_t *>(s.priv + i)[7] = R.flags | D.sflags[l] | D.wflags[l];
+  } else if (l < ne && fl) {                               // a parked env: flags of its last records
+    reinterpret_cast<uint32_t *>(s.priv + i)[7] = R.flags | fl;
   }
   if (l < ne) s.park[i] = park;
   trio_store_players(D, s, ne);                            // every player's records (cooperative)
 }
 
-// The drawing wave keeps every player's deck (img).  At odd t it takes records t - 1 and t: each
-// record's play replayed on the acting player's deck (the hand and active piles, as
+// The drawing wave keeps every player's deck (img).  It takes records in pairs r, r + 1 (r even):
+// each record's play replayed on the acting player's deck (the hand and active piles, as
 // Deck::activate does); then one pass over the turn ends of either record (discard + draws,
-// duo_turn_end: the env rng is this wave's).  Every granule a record changed goes to the storing
-// waves (deckr, dmask).
-DEV void trio_drawer(TrioLds &D, const DevState &s_glob, int steps) {
+// duo_turn_end: the env rng is this wave's).  Which granules each record changed goes to storing
+// wave B (ring granule 3, bits 16..22).
+DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw) {
   const int l = (int)threadIdx.x - 64;
-  const size_t wbase = (size_t)blockIdx.x * 64;
+  const size_t wbase = (size_t)blockIdx.x * epw;
   const DevState s = wave_view(s_glob, wbase);
   const size_t i = (size_t)l;
-  const bool live = wbase + (size_t)l < s_glob.n;
+  const bool live = l < epw && wbase + (size_t)l < s_glob.n;
   uint32_t rng = 0u;                                       // the env rng
   if (live) {
 #pragma unroll
@@ -3743,95 +3823,82 @@ DEV void trio_drawer(TrioLds &D, const DevState &s_glob, int steps) {
     }
     rng = reinterpret_cast<const uint32_t *>(s.priv + i)[0];
   }
-  D.sflags[l] = 0u;
+  uint32_t flags = 0u;                                     // hazard flags of the draws
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();                                         // B: the decks are in LDS
   PH_DECL;
-  int c3 = 0;                                              // t % 3
-  for (int t = 0; t <= steps + 1; t++) {
-    __syncthreads();                                       // X_t
-    __syncthreads();                                       // Y_t
+  TrioCnt6 cc;
+  for (int r = 0; r < steps; r += 2) {
+    const int nrec = r + 1 < steps ? 2 : 1;
+    cnt_wait(D, cc, cc.rec, (uint32_t)(r + nrec), s_glob);   // the records are written
     PH(8);
-    if ((t & 1) && t - 1 < steps) {                        // records t - 1 and t
-      const int slot[2] = {mod3_prev(c3), c3};
-      uint32_t dm[2] = {0u, 0u};
-      int agj[2] = {0, 0};
-      bool te[2] = {false, false};
+    const int slot[2] = {r & (kTrioDepth - 1), (r + 1) & (kTrioDepth - 1)};
+    uint32_t dm[2] = {0u, 0u};
+    int agj[2] = {0, 0};
+    bool te[2] = {false, false};
 #pragma unroll
-      for (int j = 0; j < 2; j++) {                        // the plays, in record order
-        if (t - 1 + j >= steps) continue;                  // (uniform)
-        const uint32_t meta = D.ring[slot[j]][1][l].w;
-        const int ag = (int)((meta >> 2) & 3u);
-        const bool rec = live && (meta & kMetaValid) && (meta & kMetaStepped);
-        agj[j] = ag;
-        te[j] = rec && (int)(meta >> 24) != ag;
-        const int a_play = (int)(D.ring[slot[j]][2][l].w & 0xffu);
-        if (rec && a_play) {                               // Deck::activate (cards.cpp:242-253)
-          uint32_t d[28];
-          uint4 old[7];
-#pragma unroll
-          for (int k = 1; k < 4; k++) {                    // (hand and active piles: granules 1..3)
-            old[k] = D.img[ag][k][l];
-            d[4 * k] = old[k].x; d[4 * k + 1] = old[k].y; d[4 * k + 2] = old[k].z; d[4 * k + 3] = old[k].w;
-          }
-          pile_add<COG_DECK_HAND>(d, a_play - 1, 0xffu);
-          pile_add<COG_DECK_ACTIVE>(d, a_play - 1, 1u);
-#pragma unroll
-          for (int k = 1; k < 4; k++) {
-            const uint4 v = make_uint4(d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]);
-            if (ne4(v, old[k])) {
-              dm[j] |= 1u << k;
-              D.img[ag][k][l] = v;
-              D.deckr[slot[j]][k][l] = v;
-            }
-          }
-        }
+    for (int j = 0; j < 2; j++) {                          // the plays, in record order
+      if (j >= nrec) continue;                             // (uniform)
+      const uint32_t meta = D.ring[slot[j]][1][l].w;
+      const int ag = (int)((meta >> 2) & 3u);
+      const bool rec = live && (meta & kMetaValid) && (meta & kMetaStepped);
+      agj[j] = ag;
+      te[j] = rec && (int)(meta >> 24) != ag;
+      const int a_play = (int)(D.ring[slot[j]][2][l].w & 0xffu);
+      if (rec && a_play) {                                 // Deck::activate (cards.cpp:242-253): hand[c]--,
+        const int bh = COG_DECK_HAND + a_play - 1, ba = COG_DECK_ACTIVE + a_play - 1;   // active[c]++ (u8)
+        uint8_t *ph = reinterpret_cast<uint8_t *>(&D.img[ag][bh >> 4][l]) + (bh & 15);
+        uint8_t *pa = reinterpret_cast<uint8_t *>(&D.img[ag][ba >> 4][l]) + (ba & 15);
+        *ph = (uint8_t)(*ph - 1u);
+        *pa = (uint8_t)(*pa + 1u);
+        dm[j] |= 1u << (bh >> 4) | 1u << (ba >> 4);
       }
-      const bool any = te[0] || te[1];                     // (at most one of them)
-      if (__builtin_amdgcn_ballot_w64(any) && any) {       // the turn end's discard + draws
-        const int j = te[1] ? 1 : 0, sl = te[1] ? slot[1] : slot[0], ag = te[1] ? agj[1] : agj[0];
-        uint4 dk[7], old[7];
-#pragma unroll
-        for (int k = 0; k < 7; k++) old[k] = dk[k] = D.img[ag][k][l];
-        const uint4 x = D.ring[sl][2][l];
-        MBits ba{x.x, x.y, x.z};
-        duo_turn_end(D, l, ag, dk, ba, rng);
-        D.ring[sl][2][l] = make_uint4(ba.w0, ba.w1, ba.w2, x.w);
-        uint32_t dd = 0;
-#pragma unroll
-        for (int k = 0; k < 7; k++)
-          if (ne4(dk[k], old[k])) {
-            dd |= 1u << k;
-            D.img[ag][k][l] = dk[k];
-            D.deckr[sl][k][l] = dk[k];
-          }
-        dm[0] |= j == 0 ? dd : 0u;
-        dm[1] |= j == 1 ? dd : 0u;
-      }
-      D.dmask[slot[0]][l] = dm[0];
-      if (t < steps) D.dmask[slot[1]][l] = dm[1];
     }
+    const bool any = te[0] || te[1];                       // (at most one of them)
+    if (__builtin_amdgcn_ballot_w64(any) && any) {         // the turn end's discard + draws
+      const int j = te[1] ? 1 : 0, sl = te[1] ? slot[1] : slot[0], ag = te[1] ? agj[1] : agj[0];
+      uint4 dk[7], old[7];
+#pragma unroll
+      for (int k = 0; k < 7; k++) old[k] = dk[k] = D.img[ag][k][l];
+      const uint4 x = D.ring[sl][2][l];
+      MBits ba{x.x, x.y, x.z};
+      duo_turn_end(D, l, ag, dk, ba, rng, flags);
+      D.ring[sl][2][l] = make_uint4(ba.w0, ba.w1, ba.w2, x.w);
+      uint32_t dd = 0;
+#pragma unroll
+      for (int k = 0; k < 7; k++)
+        if (ne4(dk[k], old[k])) {
+          dd |= 1u << k;
+          D.img[ag][k][l] = dk[k];
+        }
+      dm[0] |= j == 0 ? dd : 0u;
+      dm[1] |= j == 1 ? dd : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 2; j++)                            // (bytes 14..15 of granule 3: its last dword's
+      if (j < nrec)                                        // upper half; n_active below is the stepping wave's)
+        reinterpret_cast<uint16_t *>(&D.ring[slot[j]][3][l])[7] = (uint16_t)dm[j];
+    cnt_store(D, CNT_DRAW, (uint32_t)(r + nrec));
     PH(9);
-    c3 = mod3_next(c3);
   }
-  __syncthreads();                                         // X_{steps + 2}
   if (live) reinterpret_cast<uint32_t *>(s.priv + i)[0] = rng;   // the env rng after its last draws
   PH_FLUSH(s_glob);
+  return flags;
 }
 
-// The store phase of the trio on two waves, record t in [Y_{t+2}, X_{t+3}]: wave A (PART 0) the
-// ObsData shared block and the stored masks -- update_observation's heads of the acting player's
-// when the turn goes on (the lean step leaves them, step_lean) -- and wave B (PART 1) the decks,
-// the selected-mask record, the Info steps byte, the action, dones / agent_selection, and the
-// presampled draws (presample).  Each keeps its own images of what it stored last.
+// The store phase of the trio on two waves: wave A (PART 0) the ObsData shared block and the
+// stored masks -- update_observation's heads of the acting player's when the turn goes on (the
+// lean step leaves them, step_lean) -- and wave B (PART 1) the presampled draws (presample), the
+// selected-mask record, the Info steps byte, the action, dones / agent_selection and the decks.
+// Each keeps its own images of what it stored last.
 template <int PART>
-DEV void trio_storer(TrioLds &D, const DevState &s_glob, int steps, const uint32_t *__restrict__ rngs_glob,
-                     uint8_t *__restrict__ actions_glob) {
+DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw, const uint32_t *__restrict__ rngs_glob,
+                         uint8_t *__restrict__ actions_glob) {
   const int l = (int)(threadIdx.x & 63);
-  const size_t wbase = (size_t)blockIdx.x * 64;
+  const size_t wbase = (size_t)blockIdx.x * epw;
   const DevState s = wave_view(s_glob, wbase);
   const size_t i = (size_t)l;
-  const bool live = wbase + (size_t)l < s_glob.n;
+  const bool live = l < epw && wbase + (size_t)l < s_glob.n;
   uint8_t *__restrict__ av = actions_glob + wbase * COG_ACTION_BYTES;
   uint4 shb0 = make_uint4(0u, 0u, 0u, 0u);                 // A: ObsData 16128.. as stored
   MBits selb = {0u, 0u, 0u}, stb[4];                       // B: selected mask; A: stored masks
@@ -3840,7 +3907,7 @@ DEV void trio_storer(TrioLds &D, const DevState &s_glob, int steps, const uint32
   RegEnv E;                                                // A: update_observation's inputs and flags
   E.flags = 0u;
   E.avail = 0u;
-  uint32_t x0 = 1u;                                        // B: the sampler state at step 0
+  uint32_t x = 1u;                                         // B: the sampler state at step 0
   if (live) {
     if (PART == 0) {
       const uint4 *sh4 = reinterpret_cast<const uint4 *>(s.obs + i * COG_OBS_BYTES + COG_OBS_PHASE);
@@ -3857,67 +3924,38 @@ DEV void trio_storer(TrioLds &D, const DevState &s_glob, int steps, const uint32
       E.avail = shop_avail_of(w, (g1.y >> 8) & 0xffu, g1.z);   // (no purchase in the lean step: fixed)
     } else {
       selb = mbits_of(s.heads[5 * i]);
-      x0 = rngs_glob[wbase + (size_t)l];
+      x = rngs_glob[wbase + (size_t)l];
     }
   }
-  if (PART == 1) {
-    D.pre[0][l] = presample(x0);                           // steps 0 and 1
-    D.pre[1][l] = presample(mr_jump(x0, kPow5));
+  if (PART == 1) {                                         // steps 0..3 from the state at step 0
+#pragma unroll
+    for (int k = 0; k < kTrioLead; k++) {
+      const uint4 p = presample(x);
+      D.pre[k][l] = pre_pack(p);
+      x = p.z;
+    }
   }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();                                         // B
   PH_DECL;
-  int c3 = 1;                                              // (t - 2) % 3
-  for (int t = 0; t <= steps + 1; t++) {
-    __syncthreads();                                       // X_t
-    __syncthreads();                                       // Y_t
-    PH(5);
-    if (PART == 1 && t < 2 && t + 2 < steps)               // steps 2 and 3 from the state at step 0
-      D.pre[t & 1][l] = presample(mr_jump(x0, t ? kPow15 : kPow10));
-    if (t >= 2) {                                          // record t - 2
-      const int sl = c3;
+  // B runs two cursors: record r's part that needs no draws (the presampled draws first: the
+  // stepping wave waits for them), and record r - kTrioBLag's deck granules once drawn, so that
+  // the presampled draws never wait for the drawing wave.  A: record r once drawn.
+  constexpr int LAG = PART == 1 ? kTrioBLag : 0;
+  TrioCnt6 cc;
+  for (int r = 0; r < steps + LAG; r++) {
+    if (PART == 1 && r < steps) {                          // record r written
+      const int sl = r & (kTrioDepth - 1);
+      cnt_wait(D, cc, cc.rec, (uint32_t)(r + 1), s_glob);
+      PH(5);
       const uint4 m = D.ring[sl][1][l];
       const uint32_t meta = m.w;
       const bool rec = live && (meta & kMetaValid);
-      const int ag = (int)((meta >> 2) & 3u), na = (int)((meta >> 4) & 3u);
-      if (PART == 1 && rec && t + 2 < steps)               // step t + 2's draws: the state step t - 1
-        D.pre[t & 1][l] = presample(mr_jump(D.srng[sl][l], kPow15));   // starts at, + 15 draws
-      if (rec && PART == 0) {
-        const uint4 g0 = D.ring[sl][0][l], x = D.ring[sl][2][l];
-        MBits ba{x.x, x.y, x.z};
-        if ((int)(meta >> 24) == ag && (meta & kMetaStepped)) {   // the turn goes on: update_observation of
-          Heads h = heads_of(ba);                          // ag's stored mask (environment.cpp:252-279)
-          const uint32_t phase = g0.x & 0xffu;
-          const float r0 = __uint_as_float(g0.y), r1 = __uint_as_float(g0.z), r2 = __uint_as_float(g0.w);
-          const uint32_t n_active = (D.ring[sl][3][l].w >> 8) & 0xffu;
-          uint2 ca = cells[3];                             // (selects: no indexed registers)
-#pragma unroll
-          for (int p = 2; p >= 0; p--) ca = ag == p ? cells[p] : ca;
-          h.move = phase == COG_PHASE_MOVEMENT ? E.move_bits(ca, r0, r1, r2, n_active) : 1u;
-          h.shop = phase == COG_PHASE_BUYING ? E.shop_bits(r2) : 1u;
-          ba = bits_of(h);
-        }
-        PH(6);
-        uint8_t *ob = s.obs + i * COG_OBS_BYTES;
-        if (ne4(g0, shb0)) reinterpret_cast<uint4 *>(ob + COG_OBS_PHASE)[0] = g0;
-        shb0 = g0;
-        uint8_t *deck = deck_ptr(s, i, ag);
-        store_mask_record(reinterpret_cast<uint4 *>(deck + COG_PD_MASK), ba, mask_diff_granules(ba, selm(stb, ag)));
-        setm(stb, ag, ba);
-        if (na != ag) {
-          const uint4 y = D.ring[sl][3][l];
-          const MBits bn{y.x, y.y, y.z};
-          store_mask_record(reinterpret_cast<uint4 *>(deck_ptr(s, i, na) + COG_PD_MASK), bn,
-                            mask_diff_granules(bn, selm(stb, na)));
-          setm(stb, na, bn);
-        }
-      }
-      if (rec && PART == 1) {
-        const uint32_t dm = D.dmask[sl][l];                // deck granules that changed (drawing wave)
-        uint8_t *deck = deck_ptr(s, i, ag);
-#pragma unroll
-        for (int k = 0; k < 7; k++)
-          if ((dm >> k) & 1u) reinterpret_cast<uint4 *>(deck)[k] = D.deckr[sl][k][l];
+      const int ag = (int)((meta >> 2) & 3u);
+      if (rec && r + kTrioLead < steps)                    // step r + 4's draws: the state after step r,
+        D.pre[(r + kTrioLead) & (kTrioLead - 1)][l] = pre_pack(presample(mr_jump(D.srng[sl][l], kPow15)));
+      cnt_store(D, CNT_PRE, (uint32_t)(r + 1));            // + 15 draws (steps r + 1 .. r + 3)
+      if (rec) {
         s.info[i * COG_INFO_BYTES + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag] = (uint8_t)(meta >> 8);
         const MBits bs{m.x, m.y, m.z};
         store_mask_record(reinterpret_cast<uint4 *>(s.sel + i * COG_MASK_BYTES), bs, mask_diff_granules(bs, selb));
@@ -3931,39 +3969,90 @@ DEV void trio_storer(TrioLds &D, const DevState &s_glob, int steps, const uint32
         }
       }
     }
+    const int q = r - LAG;                                 // record q drawn
+    if (q < 0) continue;                                   // (uniform)
+    const int sl = q & (kTrioDepth - 1);
+    cnt_wait(D, cc, cc.draw, (uint32_t)(q + 1), s_glob);
+    PH(6);
+    const uint32_t meta = D.ring[sl][1][l].w;
+    const bool rec = live && (meta & kMetaValid);
+    const int ag = (int)((meta >> 2) & 3u), na = (int)((meta >> 4) & 3u);
+    if (rec && PART == 0) {
+      const uint4 g0 = D.ring[sl][0][l], xa = D.ring[sl][2][l];
+      MBits ba{xa.x, xa.y, xa.z};
+      if ((int)(meta >> 24) == ag && (meta & kMetaStepped)) {   // the turn goes on: update_observation of
+        Heads h = heads_of(ba);                            // ag's stored mask (environment.cpp:252-279)
+        const uint32_t phase = g0.x & 0xffu;
+        const float r0 = __uint_as_float(g0.y), r1 = __uint_as_float(g0.z), r2 = __uint_as_float(g0.w);
+        const uint32_t n_active = (D.ring[sl][3][l].w >> 8) & 0xffu;
+        uint2 ca = cells[3];                               // (selects: no indexed registers)
+#pragma unroll
+        for (int p = 2; p >= 0; p--) ca = ag == p ? cells[p] : ca;
+        h.move = phase == COG_PHASE_MOVEMENT ? E.move_bits(ca, r0, r1, r2, n_active) : 1u;
+        h.shop = phase == COG_PHASE_BUYING ? E.shop_bits(r2) : 1u;
+        ba = bits_of(h);
+      }
+      uint8_t *ob = s.obs + i * COG_OBS_BYTES;
+      if (ne4(g0, shb0)) reinterpret_cast<uint4 *>(ob + COG_OBS_PHASE)[0] = g0;
+      shb0 = g0;
+      uint8_t *deck = deck_ptr(s, i, ag);
+      store_mask_record(reinterpret_cast<uint4 *>(deck + COG_PD_MASK), ba, mask_diff_granules(ba, selm(stb, ag)));
+      setm(stb, ag, ba);
+      if (na != ag) {
+        const uint4 y = D.ring[sl][3][l];
+        const MBits bn{y.x, y.y, y.z};
+        store_mask_record(reinterpret_cast<uint4 *>(deck_ptr(s, i, na) + COG_PD_MASK), bn,
+                          mask_diff_granules(bn, selm(stb, na)));
+        setm(stb, na, bn);
+      }
+    }
+    if (rec && PART == 1) {                                // deck granules the record changed, from img
+      const uint32_t dm = D.ring[sl][3][l].w >> 16;
+      uint4 *deck = reinterpret_cast<uint4 *>(deck_ptr(s, i, ag));
+#pragma unroll
+      for (int k = 0; k < 7; k++)
+        if ((dm >> k) & 1u) deck[k] = D.img[ag][k][l];
+    }
+    cnt_store(D, PART == 0 ? CNT_STA : CNT_STB, (uint32_t)(q + 1));
     PH(13);
-    c3 = mod3_next(c3);
   }
   // A: the stored-mask bit vectors as stored (the epilogue's; the drawing wave's turn ends
-  // included), and its hazard flags (update_observation's lookups) for the stepping wave to merge
+  // included), once the stepping wave no longer reads them
   if (PART == 0) {
+    cnt_wait(D, cc, cc.rec, (uint32_t)steps + 1u, s_glob);
     if (live) {
 #pragma unroll
       for (int p = 0; p < 4; p++) D.heads[p][l] = mbits_u4(stb[p]);
     }
-    D.wflags[l] = E.flags;
   }
-  __syncthreads();                                         // X_{steps + 2}
   PH_FLUSH(s_glob);
+  return E.flags;                                          // (A: update_observation's lookups)
 }
 
-// four waves per workgroup: stepping, drawing and two storing waves
+// four waves per workgroup: stepping, drawing and two storing waves, for epw (32 or 64) envs: lanes
+// epw.. idle (trio_epw: half-empty waves fill all 256 CUs at 8,192 envs).  The drawing and storing
+// waves leave their hazard flags in flg[] and count themselves done in cnt[FIN]; the stepping wave
+// waits for all three before its epilogue.
 template <int SRC>
-__global__ void __launch_bounds__(256) k_env_rollout_trio(DevState s, int steps, uint32_t *__restrict__ rngs,
+__global__ void __launch_bounds__(256) k_env_rollout_trio(DevState s, int steps, int epw, uint32_t *__restrict__ rngs,
                                                           uint8_t *__restrict__ actions_out) {
   __shared__ TrioLds D;
   const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform
-  uid_tab_fill(D.tab);
+  if (threadIdx.x < 64) D.flg[threadIdx.x] = 0u;
+  if (threadIdx.x < kTrioCnts) D.cnt[threadIdx.x] = 0u;
+  uid_tab_fill(D.tab);                                     // (ends on a barrier)
   if (role == 0) {
     __builtin_amdgcn_s_setprio(3);
-    trio_stepper<SRC>(D, s, steps, rngs);
-  } else if (role == 1) {
-    trio_drawer(D, s, steps);
-  } else if (role == 2) {
-    trio_storer<0>(D, s, steps, rngs, actions_out);
-  } else {
-    trio_storer<1>(D, s, steps, rngs, actions_out);
+    trio_stepper<SRC>(D, s, steps, epw, rngs);
+    return;
   }
+  uint32_t flags;
+  if (role == 1) flags = trio_drawer(D, s, steps, epw);
+  else if (role == 2) flags = trio_storer<0>(D, s, steps, epw, rngs, actions_out);
+  else flags = trio_storer<1>(D, s, steps, epw, rngs, actions_out);
+  const int l = (int)(threadIdx.x & 63);
+  if (flags) __hip_atomic_fetch_or(&D.flg[l], flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (l == 0) __hip_atomic_fetch_add(&D.cnt[CNT_FIN], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // The episode ends k_env_rollout_duo parked: a wave with a parked lane runs k_env_rollout's
@@ -4278,6 +4367,16 @@ static int rollout_kind(size_t n, int mask_source, bool defer_ok) {
   return n <= 16384 ? RK_DUO : n <= 32768 ? RK_PIPE : RK_WAVE;
 }
 int rollout_kind_of(size_t n, int mask_source, bool defer_ok) { return rollout_kind(n, mask_source, defer_ok); }
+// envs per trio workgroup ($COG_TRIO_EPW = 32 | 64 forces it)
+int trio_epw(size_t n) {
+  static const int forced = [] {
+    const char *e = getenv("COG_TRIO_EPW");
+    return e && *e ? atoi(e) : 0;
+  }();
+  if (forced == 32 || forced == 64) return forced;
+  (void)n;
+  return 64;
+}
 int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions, void *stream,
                    bool defer_ok) {
   if (!s.n || steps <= 0) return 0;
@@ -4295,7 +4394,9 @@ int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rn
       hipLaunchKernelGGL((k_env_rollout_duo<MASK_STORED>), g, dim3(128), 0, st, sd, steps, d_rng, d_actions);
       hipLaunchKernelGGL((k_env_fixup<MASK_STORED>), g, dim3(64), 0, st, sd, steps, d_rng, d_actions);
     } else if (kind == RK_TRIO) {                          // selected masks, >= 3 players
-      hipLaunchKernelGGL((k_env_rollout_trio<MASK_SELECTED>), g, dim3(256), 0, st, sd, steps, d_rng, d_actions);
+      const int epw = trio_epw(s.n);
+      hipLaunchKernelGGL((k_env_rollout_trio<MASK_SELECTED>), dim3(blocks_for(s.n, epw)), dim3(256), 0, st, sd, steps,
+                         epw, d_rng, d_actions);
       hipLaunchKernelGGL((k_env_fixup<MASK_SELECTED>), g, dim3(64), 0, st, sd, steps, d_rng, d_actions);
     } else {
       hipLaunchKernelGGL((k_env_rollout_duo<MASK_SELECTED>), g, dim3(128), 0, st, sd, steps, d_rng, d_actions);

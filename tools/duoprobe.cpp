@@ -63,7 +63,8 @@ int main(int argc, char **argv) {
       // drawing, storing A, storing B).  Each wave's PH slots (cog_engine.hip): its phase names below.
       const char *trio_env = getenv("COG_TRIO");
       const int wpg = (trio_env && *trio_env == '0') ? 2 : 4;
-      const size_t waves = (size_t)wpg * ((n + 63) / 64);
+      const size_t epw = wpg == 4 ? (size_t)cog::trio_epw(n) : 64;
+      const size_t waves = (size_t)wpg * ((n + epw - 1) / epw);
       constexpr int K = 16;
       unsigned long long *d;
       if (hipMalloc(&d, waves * K * sizeof(unsigned long long)) != hipSuccess) return 1;
