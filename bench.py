@@ -18,10 +18,10 @@ the bytes a one-launch-per-step run leaves (tests/test_gpu_rollout.py).  No host
 max/sum of scalars (gloo).
 
 Also reported (rank 0; the extra lines only at N=1, so a scaling run stays short):
-  roofline       the dominant kernel k_env_rollout against its store bound (bound "l2-store":
-                 the per-step output stores through L2, roofline() below); `hbm` holds the
-                 counter-measured HBM traffic (FETCH x 2 + WRITE, gfx950 corrections) and SURVEY
-                 8d's 800 B/env-step figure, `valu_issue` the VALU rate against the SIMDs' peak.
+  roofline       the dominant kernel (the trio rollout) against HBM by SURVEY 8d's 800 B/env-step
+                 (roofline() below), with the counter-measured HBM traffic of the same launch shape
+                 (FETCH x 2 + WRITE, gfx950 corrections), round 3's L2 store model as a record and
+                 `valu_issue` the VALU rate against the SIMDs' peak.
   shard_sizes    rollout us/step at the N=1 batch (65,536 on one GPU) and the N=8 shard (8,192)
   per_launch     one kernel launch per step (k_env_step<selected>)
   host_loop      the reference's numpy loop through the host API at C2 (256, EASY) and the C4
@@ -344,28 +344,28 @@ KERNEL_LABEL = {"wave": "k_env_rollout<selected>", "pipe": "k_env_rollout_pipe<s
                 "trio": "k_env_rollout_trio<selected> + k_env_fixup<selected>"}
 
 
-def roofline(prof, n, k_chunk, launch_s, kind="wave"):
-    """The dominant kernel -- the persistent rollout that runs a shard of n envs (`kind`: wave,
-    pipe, duo or trio, cog_rollout_kind) -- against what bounds it: its per-step output stores through L2
-    (profiles/r03_store_bound.txt).  Every step stores the ~6.2 changed 16-B granules of each env's
-    records (ObsData tail, selected mask, Info byte, action); at 65,536 envs an XCD's share of those
-    lines exceeds its 4 MiB L2, so about half the stores miss and each costs a fabric write-back.
-    Store bound of one launch: T_store = hits x c_hit + misses x c_miss, with the launch's L2 write
-    hits / misses from a rocprofv3 --pmc pass of this exact engine source AT THIS LAUNCH SHAPE (n
-    envs, k steps per launch: profiles/pmc_profile.json `rollouts`) and c_hit / c_miss the measured
-    cost of a scattered 16-B store that hits / misses L2 on this chip (tools/storeprobe.hip).
-    achieved = env-steps/s of the launch timed here (HIP events); peak = env-steps/s if the launch
-    took T_store; frac = T_store / launch time.  Beside it: the counter HBM traffic of the same
-    shape and the VALU issue rate.  No profile of this shape: traffic, peak and frac are null."""
+def roofline(prof, n, k_chunk, launch_s, kind="trio"):
+    """The dominant kernel -- the persistent rollout that runs a shard of n envs (`kind`: trio, wave,
+    pipe or duo, cog_rollout_kind) -- against HBM, SURVEY 8d's way: achieved = 800 algorithmic bytes
+    per env-step (the bytes a one-launch-per-step sample + step would move) x the launch's
+    env-steps / the launch time (HIP events), peak = 8 TB/s.  The rollout keeps every env's state on
+    chip between steps, so it moves far fewer bytes than that and frac can exceed 1; `traffic` is
+    what it does move, the HBM bytes of a rocprofv3 --pmc pass of this exact engine source AT THIS
+    LAUNCH SHAPE (n envs, k steps per launch, same kernel: profiles/pmc_profile.json `rollouts`;
+    FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 corrections), with counter_frac = traffic / time / peak.
+    store_model: round 3's L2 store-cost model of the same launch (hits x c_hit + misses x c_miss,
+    tools/storeprobe.hip); the trio beats it (frac > 1), so it is no bound -- kept as a record.  No
+    profile of this shape: traffic and store_model are null."""
+    alg = STEP_BYTES * n * k_chunk
+    out = {"bound": "hbm", "kernel": KERNEL_LABEL.get(kind, kind), "rollout_kind": kind, "unit": "GB/s",
+           "achieved": alg / launch_s / 1e9, "peak": HBM_PEAK_GBS, "frac": alg / launch_s / 1e9 / HBM_PEAK_GBS,
+           "traffic": None, "algorithmic_bytes_per_launch": alg, "env_steps_per_s": n * k_chunk / launch_s,
+           "kernel_ms": launch_s * 1e3, "steps_per_launch": k_chunk, "envs_per_launch": n, "store_model": None,
+           "note": "achieved / frac use SURVEY 8d's 800 B per env-step; the rollout keeps the state on chip, "
+                   "so its real HBM bytes are `traffic` (counter_frac); it is bound by the stepping wave's "
+                   "instruction latency (DESIGN.md 6)"}
     waves = (n + 63) // 64
     valu_peak = N_SIMD * CLOCK_HZ / VALU_CYC                # wave64 VALU instructions per second
-    out = {"bound": "l2-store", "kernel": KERNEL_LABEL.get(kind, kind), "rollout_kind": kind, "unit": "env-steps/s",
-           "achieved": n * k_chunk / launch_s, "peak": None, "frac": None, "traffic": None,
-           "kernel_ms": launch_s * 1e3, "steps_per_launch": k_chunk, "envs_per_launch": n}
-    alg = STEP_BYTES * n * k_chunk
-    out["hbm"] = {"survey_8d_bytes_per_launch": alg, "survey_8d_GBs": alg / launch_s / 1e9,
-                  "note": "800 B/env-step (SURVEY 8d) assumes every step reads its state from HBM; "
-                          "the rollout keeps it on-chip, so this rate can exceed the HBM peak"}
     e = ((prof or {}).get("rollouts") or {}).get("%d:%d" % (n, k_chunk))
     if e and e.get("kind") != kind:
         e = None                                          # profiled with another rollout kernel
@@ -373,26 +373,21 @@ def roofline(prof, n, k_chunk, launch_s, kind="wave"):
     l2 = (e or {}).get("l2_per_launch")
     if l2 and sc:
         t_store = l2["hits"] * sc["c_hit_s"] + l2["misses"] * sc["c_miss_s"]
-        out.update(peak=n * k_chunk / t_store, frac=t_store / launch_s,
-                   store_model={"l2_write_requests_per_env_step": l2["writes"] / n / k_chunk,
-                                "l2_hits_per_launch": l2["hits"], "l2_misses_per_launch": l2["misses"],
-                                "l2_hit_rate": l2["hits"] / max(1.0, l2["hits"] + l2["misses"]),
-                                "fabric_write_requests_per_launch": l2.get("fabric_write_requests"),
-                                "c_hit_s": sc["c_hit_s"], "c_miss_s": sc["c_miss_s"],
-                                "t_store_s": t_store, "t_kernel_s": launch_s})
-        if kind != "wave":
-            out["note"] = ("shards of <= 32,768 envs keep their written lines in L2: the store bound is "
-                           "far from the launch time, which the stepping wave's instruction latency sets "
-                           "(DESIGN.md 7)")
-    else:
-        out["note"] = "no PMC profile of this engine source at %d envs x %d steps (%s; tools/pmc_profile.py): " \
-                      "store bound unknown" % (n, k_chunk, kind)
+        out["store_model"] = {"t_store_s": t_store, "frac": t_store / launch_s, "peak_env_steps_per_s": n * k_chunk / t_store,
+                              "l2_write_requests_per_env_step": l2["writes"] / n / k_chunk,
+                              "l2_hits_per_launch": l2["hits"], "l2_misses_per_launch": l2["misses"],
+                              "l2_hit_rate": l2["hits"] / max(1.0, l2["hits"] + l2["misses"]),
+                              "fabric_write_requests_per_launch": l2.get("fabric_write_requests"),
+                              "c_hit_s": sc["c_hit_s"], "c_miss_s": sc["c_miss_s"]}
+    if not e:
+        out["note"] += "; no PMC profile of this engine source at %d envs x %d steps (%s; tools/pmc_profile.py): " \
+                       "traffic unknown" % (n, k_chunk, kind)
     if e and e.get("bytes_per_launch") is not None:
         tr = e["bytes_per_launch"] + ((e.get("companion") or {}).get("bytes_per_launch") or 0.0)
         out["traffic"] = tr
-        out["hbm"]["counter_GBs"] = tr / launch_s / 1e9
-        out["hbm"]["counter_frac"] = tr / launch_s / 1e9 / HBM_PEAK_GBS
-        out["hbm"]["counter_bytes_per_env_step"] = tr / n / k_chunk
+        out["counter_GBs"] = tr / launch_s / 1e9
+        out["counter_frac"] = tr / launch_s / 1e9 / HBM_PEAK_GBS
+        out["counter_bytes_per_env_step"] = tr / n / k_chunk
     pw = (e or {}).get("per_wave_step") or {}
     if pw.get("valu"):
         achieved = pw["valu"] * waves * k_chunk / launch_s
@@ -402,8 +397,8 @@ def roofline(prof, n, k_chunk, launch_s, kind="wave"):
             "issue_quads_per_wave_step": pw.get("active_inst_any"), "wait_quads_per_wave_step": pw.get("wait_any"),
             "wave_quads_per_wave_step": pw.get("wave_cycles"),
             "note": "peak = 1,024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU; per 64-env wave and step (the duo / trio / "
-                    "pipe: every wave of the workgroup); not the bound at 65,536 envs, where a lone wave of this "
-                    "kernel uses about a quarter of its SIMD's VALU rate"}
+                    "pipe: every wave of the workgroup); not the bound: the stepping wave's dependent "
+                    "instruction latency sets the step"}
     return out
 
 

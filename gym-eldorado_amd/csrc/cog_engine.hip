@@ -3560,11 +3560,13 @@ __global__ void __launch_bounds__(128) k_env_rollout_duo(DevState s, int steps, 
 //
 // record t: 0 ObsData 16128.. (phase, resources; the lean step never changes the shop), 1 selected-
 // mask bits + meta, 2 the acting player's stored-mask bits (saved mask at a turn end: the drawing
-// wave adds the drawn cards) + action byte 0, 3 the next player's stored-mask bits + n_active of
-// the acting player << 8 + the deck granules the record changed << 16 (drawing wave).  The
+// wave adds the drawn cards) + action byte 0 + n_active of the acting player << 8 + the deck
+// granules the record changed << 16 (drawing wave).  The next player's stored mask changes only at a
+// turn end, by fixed heads (step_lean), so storing wave A derives it from its own image.  The
 // neighbourhood caches never change in the lean step (no moves): the stepping wave and storing wave
-// A keep their own copies, and the epilogue does not store them.
-constexpr int kTrioRingG = 4;
+// A keep their own copies, and the epilogue does not store them.  The stepping wave's player
+// counters go to LDS only at a turn end (the drawing wave's) and at a park or the end (the epilogue's).
+constexpr int kTrioRingG = 3;
 constexpr int kTrioDepth = 8;                              // ring slots (records in flight)
 constexpr int kTrioLead = 4;                               // presampled draws: steps ahead of the record
 constexpr int kTrioBLag = 2;                               // storing wave B: deck cursor behind its front
@@ -3713,6 +3715,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
         srng = srng0;
         duo_store_env_private<true>(s, i, R);
         rngs[i] = srng;
+        D.pl[ag][l] = pack_player(R.P);                    // (the epilogue's)
         park = (uint32_t)t | kParkRedo;
         live = false;
       } else {
@@ -3721,7 +3724,6 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
         if (finish) R.set_done(1u);
         ended = was_done || finish;
         PH(0);
-        D.pl[ag][l] = pack_player(R.P);                    // (the drawing wave's, at a turn end)
       }
     }
     uint4(*ring)[64] = D.ring[sl];
@@ -3729,21 +3731,13 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     if (live) {
       ag1 = (int)R.agent();
       na1 = (int)next_player((uint32_t)ag1, R.n_players());
-      const MBits bs = bits_of(R.sel), ba = bits_of(R.sta), bn = bits_of(R.stn);
-      const uint32_t info = (R.info_steps >> (8 * ag)) & 0xffu;
-      const uint32_t meta = kMetaValid | (uint32_t)ag << 2 | (uint32_t)na << 4 | (uint32_t)na1 << 6 | info << 8 |
-                            (ended ? kMetaEnded : 0u) | (stepped ? kMetaStepped : 0u) | (uint32_t)ag1 << 24;
-      ring[0][l] = make_uint4(R.sh[0], R.sh[1], R.sh[2], R.sh[3]);
-      ring[1][l] = make_uint4(bs.w0, bs.w1, bs.w2, meta);
-      ring[2][l] = make_uint4(ba.w0, ba.w1, ba.w2, (uint32_t)act[0]);   // (lean: the other heads 0)
-      ring[3][l] = make_uint4(bn.w0, bn.w1, bn.w2, (R.P.n_active & 0xffu) << 8);
-      D.srng[sl][l] = srng;
-    } else {
-      ring[1][l] = make_uint4(0u, 0u, 0u, 0u);             // no record
     }
-    cnt_store(D, CNT_REC, (uint32_t)(t + 1));
-    PH(1);
     const bool tc = live && ag1 != ag;                     // turn change: ag1 == na acts next
+    // the new agent's records (hand, counters) and the next player's (stored mask, n_active), once
+    // the drawing wave is past their last turn ends; read ahead of the record's stores, so that
+    // their latency overlaps them
+    uint4 hd1 = make_uint4(0u, 0u, 0u, 0u), hd2 = hd1, pla = hd1, hdn = hd1;
+    uint32_t pln_y = 0u;
     if (__builtin_amdgcn_ballot_w64(tc)) {
       int need = -1;                                       // the later of ag1's and na1's last turn ends
 #pragma unroll
@@ -3759,23 +3753,43 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
         cnt_wait(D, cc, cc.draw, (uint32_t)(t - dmin + 1), s_glob);
       }
       if (tc) {
-#pragma unroll
-        for (int p = 0; p < 4; p++) tend[p] = p == ag ? t : tend[p];
-#pragma unroll                                             // its hand from the drawing wave's deck
-        for (int k = 1; k < 3; k++) {
-          const uint4 v = D.img[ag1][k][l];
-          R.d[4 * k] = v.x; R.d[4 * k + 1] = v.y; R.d[4 * k + 2] = v.z; R.d[4 * k + 3] = v.w;
-        }
-        R.P = unpack_player(D.pl[ag1][l]);
-        R.cells_a = R.cells_n;
-        R.sta = R.stn;
-        R.stn = heads_of(mbits_of(D.heads[na1][l]));
-        uint2 cn = cells[3];                               // (selects: no indexed registers)
-#pragma unroll
-        for (int p = 2; p >= 0; p--) cn = na1 == p ? cells[p] : cn;
-        R.cells_n = cn;
-        R.na_active = (D.pl[na1][l].y >> 16) & 0xffu;
+        hd1 = D.img[ag1][1][l];
+        hd2 = D.img[ag1][2][l];
+        pla = D.pl[ag1][l];
+        hdn = D.heads[na1][l];
+        pln_y = D.pl[na1][l].y;
       }
+    }
+    if (live) {
+      // the acting player's counters: the drawing wave's at its turn end, the epilogue's at a park
+      if (tc || ended) D.pl[ag][l] = pack_player(R.P);
+      const MBits bs = bits_of(R.sel), ba = bits_of(R.sta);
+      const uint32_t info = (R.info_steps >> (8 * ag)) & 0xffu;
+      const uint32_t meta = kMetaValid | (uint32_t)ag << 2 | (uint32_t)na << 4 | (uint32_t)na1 << 6 | info << 8 |
+                            (ended ? kMetaEnded : 0u) | (stepped ? kMetaStepped : 0u) | (uint32_t)ag1 << 24;
+      ring[0][l] = make_uint4(R.sh[0], R.sh[1], R.sh[2], R.sh[3]);
+      ring[1][l] = make_uint4(bs.w0, bs.w1, bs.w2, meta);
+      ring[2][l] = make_uint4(ba.w0, ba.w1, ba.w2, (uint32_t)act[0] | (R.P.n_active & 0xffu) << 8);
+      D.srng[sl][l] = srng;
+    } else {
+      ring[1][l] = make_uint4(0u, 0u, 0u, 0u);             // no record
+    }
+    cnt_store(D, CNT_REC, (uint32_t)(t + 1));
+    PH(1);
+    if (tc) {
+#pragma unroll
+      for (int p = 0; p < 4; p++) tend[p] = p == ag ? t : tend[p];
+      R.d[4] = hd1.x; R.d[5] = hd1.y; R.d[6] = hd1.z; R.d[7] = hd1.w;   // its hand from the drawing
+      R.d[8] = hd2.x; R.d[9] = hd2.y; R.d[10] = hd2.z; R.d[11] = hd2.w; // wave's deck
+      R.P = unpack_player(pla);
+      R.cells_a = R.cells_n;
+      R.sta = R.stn;
+      R.stn = heads_of(mbits_of(hdn));
+      uint2 cn = cells[3];                                 // (selects: no indexed registers)
+#pragma unroll
+      for (int p = 2; p >= 0; p--) cn = na1 == p ? cells[p] : cn;
+      R.cells_n = cn;
+      R.na_active = (pln_y >> 16) & 0xffu;
     }
     if (live && ended) {                                   // hand the env to k_env_fixup
       duo_store_env_private<true>(s, i, R);
@@ -3787,6 +3801,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     na = na1;
     PH(3);
   }
+  if (live) D.pl[ag][l] = pack_player(R.P);               // (the epilogue's)
   cnt_store(D, CNT_REC, (uint32_t)steps + 1u);             // the loop is over (storing wave A's epilogue)
   cnt_wait(D, cc, cc.fin, 3u, s_glob);                        // the other waves are done
   PH_FLUSH(s_glob);
@@ -3875,9 +3890,10 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
       dm[1] |= j == 1 ? dd : 0u;
     }
 #pragma unroll
-    for (int j = 0; j < 2; j++)                            // (bytes 14..15 of granule 3: its last dword's
-      if (j < nrec)                                        // upper half; n_active below is the stepping wave's)
-        reinterpret_cast<uint16_t *>(&D.ring[slot[j]][3][l])[7] = (uint16_t)dm[j];
+    for (int j = 0; j < 2; j++)                            // (bytes 14..15 of granule 2: its last dword's
+      if (j < nrec)                                        // upper half; the action and n_active below are
+                                                           // the stepping wave's)
+        reinterpret_cast<uint16_t *>(&D.ring[slot[j]][2][l])[7] = (uint16_t)dm[j];
     cnt_store(D, CNT_DRAW, (uint32_t)(r + nrec));
     PH(9);
   }
@@ -3960,7 +3976,7 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
         const MBits bs{m.x, m.y, m.z};
         store_mask_record(reinterpret_cast<uint4 *>(s.sel + i * COG_MASK_BYTES), bs, mask_diff_granules(bs, selb));
         selb = bs;
-        reinterpret_cast<uint2 *>(av + i * COG_ACTION_BYTES)[0] = make_uint2(D.ring[sl][2][l].w, 0u);   // (lean: heads 1-4 are 0)
+        reinterpret_cast<uint2 *>(av + i * COG_ACTION_BYTES)[0] = make_uint2(D.ring[sl][2][l].w & 0xffu, 0u);   // (lean: heads 1-4 are 0)
         if (!(meta & kMetaEnded)) {                        // dones[i] = 0, agent_selection[i]
           const uint32_t agent = meta >> 24;               // (an ended episode: k_env_fixup)
           if (out & 0xffu) s.done[i] = 0;
@@ -3984,7 +4000,7 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
         Heads h = heads_of(ba);                            // ag's stored mask (environment.cpp:252-279)
         const uint32_t phase = g0.x & 0xffu;
         const float r0 = __uint_as_float(g0.y), r1 = __uint_as_float(g0.z), r2 = __uint_as_float(g0.w);
-        const uint32_t n_active = (D.ring[sl][3][l].w >> 8) & 0xffu;
+        const uint32_t n_active = (xa.w >> 8) & 0xffu;
         uint2 ca = cells[3];                               // (selects: no indexed registers)
 #pragma unroll
         for (int p = 2; p >= 0; p--) ca = ag == p ? cells[p] : ca;
@@ -3998,16 +4014,18 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
       uint8_t *deck = deck_ptr(s, i, ag);
       store_mask_record(reinterpret_cast<uint4 *>(deck + COG_PD_MASK), ba, mask_diff_granules(ba, selm(stb, ag)));
       setm(stb, ag, ba);
-      if (na != ag) {
-        const uint4 y = D.ring[sl][3][l];
-        const MBits bn{y.x, y.y, y.z};
+      if ((int)(meta >> 24) != ag && (meta & kMetaStepped)) {   // a turn end: the new agent's stored mask
+        Heads hn = heads_of(selm(stb, na));                // gets update_observation's INACTIVE-phase
+        hn.move = 1u;                                      // heads (step_lean)
+        hn.shop = 1u;
+        const MBits bn = bits_of(hn);
         store_mask_record(reinterpret_cast<uint4 *>(deck_ptr(s, i, na) + COG_PD_MASK), bn,
                           mask_diff_granules(bn, selm(stb, na)));
         setm(stb, na, bn);
       }
     }
     if (rec && PART == 1) {                                // deck granules the record changed, from img
-      const uint32_t dm = D.ring[sl][3][l].w >> 16;
+      const uint32_t dm = D.ring[sl][2][l].w >> 16;
       uint4 *deck = reinterpret_cast<uint4 *>(deck_ptr(s, i, ag));
 #pragma unroll
       for (int k = 0; k < 7; k++)
@@ -4337,12 +4355,13 @@ static void rollout_launch(const DevState &s, int mask_source, int steps, uint32
 }
 // Which rollout kernels run a shard of n envs (measured on MI355X, device us/step in 1,000-step
 // launches, profiles/r03_rollout_kinds.txt, profiles/r04e_trio_ab.txt):
-//   n <= 32,768, selected masks, >= 3 players: trio (k_env_rollout_trio + k_env_fixup: 1.96 at
-//                8,192 and 16,384, 2.08 at 32,768, against duo 2.45 / pipe 2.75)
-//   n <= 16,384  duo   (k_env_rollout_duo + k_env_fixup: 2.47-2.49 against pipe 2.65-2.68)
-//   n <= 32,768  pipe  (k_env_rollout_pipe: 2.75-2.76 against duo 2.96)
-//   larger       wave  (k_env_rollout: 3.91-3.96 against duo 4.0-4.7, trio 4.9: its 75 KB of LDS
-//                admit two workgroups per CU, so 1,024 of them run in two rounds)
+//   selected masks, >= 3 players: trio at every size (k_env_rollout_trio + k_env_fixup,
+//                profiles/r04p_trio_sweep.txt: 1.48 at 8,192-24,576, 1.93 at 32,768, 2.97 at 65,536
+//                against duo 2.46 at 8,192, pipe 2.75 at 32,768 and wave 3.52 / 4.12 at 32,768 /
+//                65,536; 20-step launches at 65,536: 84.7 against 104.0 us)
+//   otherwise    n <= 16,384 duo (k_env_rollout_duo + k_env_fixup: 2.47-2.49 against pipe 2.65-2.68),
+//                n <= 32,768 pipe (k_env_rollout_pipe: 2.75-2.76 against duo 2.96), larger wave
+//                (k_env_rollout: 3.91-3.96 against duo 4.0-4.7)
 // Above 16,384 envs the chip's shader clock drops (2.34 -> 2.08 GHz measured by s_memtime at the
 // same cycles per step), and the duo's storing wave costs more work per env-step than its
 // hand-off saves, so the leaner kernels win there.  $COG_ROLLOUT = duo | pipe | wave forces one
@@ -4363,7 +4382,7 @@ static int rollout_kind(size_t n, int mask_source, bool defer_ok) {
   }();
   const bool trio = defer_ok && mask_source == MASK_SELECTED && trio_on();
   if (forced != RK_AUTO) return forced == RK_DUO && trio ? (int)RK_TRIO : forced;
-  if (trio && n <= 32768) return RK_TRIO;
+  if (trio) return RK_TRIO;
   return n <= 16384 ? RK_DUO : n <= 32768 ? RK_PIPE : RK_WAVE;
 }
 int rollout_kind_of(size_t n, int mask_source, bool defer_ok) { return rollout_kind(n, mask_source, defer_ok); }
@@ -4395,8 +4414,10 @@ int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rn
       hipLaunchKernelGGL((k_env_fixup<MASK_STORED>), g, dim3(64), 0, st, sd, steps, d_rng, d_actions);
     } else if (kind == RK_TRIO) {                          // selected masks, >= 3 players
       const int epw = trio_epw(s.n);
-      hipLaunchKernelGGL((k_env_rollout_trio<MASK_SELECTED>), dim3(blocks_for(s.n, epw)), dim3(256), 0, st, sd, steps,
-                         epw, d_rng, d_actions);
+      const dim3 gt(blocks_for(s.n, epw));
+      // (k_env_fixup inside the trio launch, for shards of one workgroup per CU, was tried: no gain,
+      // its registers slowed the trio's waves, profiles/r04t_trio_fused.txt)
+      hipLaunchKernelGGL((k_env_rollout_trio<MASK_SELECTED>), gt, dim3(256), 0, st, sd, steps, epw, d_rng, d_actions);
       hipLaunchKernelGGL((k_env_fixup<MASK_SELECTED>), g, dim3(64), 0, st, sd, steps, d_rng, d_actions);
     } else {
       hipLaunchKernelGGL((k_env_rollout_duo<MASK_SELECTED>), g, dim3(128), 0, st, sd, steps, d_rng, d_actions);

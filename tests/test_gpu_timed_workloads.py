@@ -6,8 +6,9 @@ rank's shard at N = 2, 4 and 8 (`shard(65536, N-1, N)`: 32,768 / 16,384 / 8,192 
 and driven by `runner.rollout` in the two launch shapes the bench uses:
   - chunk 20: a 5-step launch (the driver's `--warmup 5`), then 20-step launches (`--steps 20`);
   - chunk 1000: 205 steps, then one 1,000-step launch (bench's default shape).
-The kernels are the bench's (cog_engine.hip rollout_kind): 32,768, 16,384 and 8,192 envs the trio
-rollout (k_env_rollout_trio + k_env_fixup: the deferred turn end), 65,536 k_env_rollout.
+The kernels are the bench's (cog_engine.hip rollout_kind): the trio rollout at every one of these
+sizes (k_env_rollout_trio + k_env_fixup: the deferred turn end); at 65,536 its 1,024 workgroups
+run in two rounds.
 After 1,205 steps ALL envs are compared with a threaded oracle run of the reference runner loop
 (`sample(selected_action_masks); step(actions)`, benchmarks/benchmarks.py:47-51,
 include/runner.h:33-62): every named field of ObsData / ActionMask / Info, rewards, dones,
