@@ -3567,7 +3567,10 @@ __global__ void __launch_bounds__(128) k_env_rollout_duo(DevState s, int steps, 
 // A keep their own copies, and the epilogue does not store them.  The stepping wave's player
 // counters go to LDS only at a turn end (the drawing wave's) and at a park or the end (the epilogue's).
 constexpr int kTrioRingG = 3;
-constexpr int kTrioDepth = 8;                              // ring slots (records in flight)
+#ifndef COG_TRIO_DEPTH                                     // (diagnostic builds: tools/r04/gpu_depth.sh)
+#define COG_TRIO_DEPTH 8
+#endif
+constexpr int kTrioDepth = COG_TRIO_DEPTH;                 // ring slots (records in flight)
 constexpr int kTrioLead = 4;                               // presampled draws: steps ahead of the record
 constexpr int kTrioBLag = 2;                               // storing wave B: deck cursor behind its front
 enum TrioCnt : int { CNT_REC = 0, CNT_DRAW, CNT_STA, CNT_STB, CNT_PRE, CNT_FIN, kTrioCnts };
@@ -3584,6 +3587,7 @@ struct TrioLds {
   UidEntry tab[kUidTab];
 };
 static_assert(sizeof(TrioLds) <= 75520, "two trio workgroups per CU (measured: 78,336 B admit one)");
+static_assert((kTrioDepth & (kTrioDepth - 1)) == 0 && kTrioDepth >= 4, "ring slots: a power of two");
 
 // A wave keeps the counters it last read (wave-uniform, in SGPRs) and reads them again -- all six
 // in one round trip -- only when the one it needs is short: the counters only grow, and what an
