@@ -467,10 +467,10 @@ def main():
         extras["shard_sizes"] = {"us_per_step_at_%d" % n: launch_s / k_chunk * 1e6 if k_chunk >= 1000 else
                                  us_per_step(cg, n, dev),
                                  "us_per_step_at_%d" % N_SHARD8: us_per_step(cg, N_SHARD8, dev),
-                                 "note": "rollout device time per step, 1,000-step launches; shards of <= 32,768 "
-                                         "envs (the N=8 shard: 8,192 = 128 workgroups) take the trio rollout: "
-                                         "a stepping wave, a wave for the deferred turn ends' draws and a wave "
-                                         "issuing the store phase per workgroup"}
+                                 "note": "rollout device time per step, 1,000-step launches; every shard size "
+                                         "takes the trio rollout (4 waves per 64 envs: stepping, drawing and two "
+                                         "storing waves; the N=8 shard of 8,192 envs is 128 workgroups, 65,536 "
+                                         "envs are 1,024 in two rounds of two per CU)"}
         # one kernel launch per step (the runner's step() path)
         pl_steps = 500
         runner.set_chunk(1)
