@@ -3103,6 +3103,8 @@ __global__ void __launch_bounds__(128) k_env_rollout_pipe(DevState s, int steps,
   __shared__ OutRing O;
   const size_t base = (size_t)blockIdx.x * 64;
   const int ne = (int)min((size_t)64, s.n - base);
+  // (roles rotated per workgroup, so that a CU's two workgroups could not put both stepping waves
+  // on one SIMD, measured the same: profiles/r04y_trio_role_rotation.txt)
   const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform
   uid_tab_fill(L.tab);
   uint32_t park = kParkNone;
@@ -3508,6 +3510,8 @@ template <int SRC>
 __global__ void __launch_bounds__(128) k_env_rollout_duo(DevState s, int steps, uint32_t *__restrict__ rngs,
                                                          uint8_t *__restrict__ actions_out) {
   __shared__ DuoLds D;
+  // (roles rotated per workgroup, so that a CU's two workgroups could not put both stepping waves
+  // on one SIMD, measured the same: profiles/r04y_trio_role_rotation.txt)
   const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform
   uid_tab_fill(D.tab);
   if (role == 0) {
@@ -3631,7 +3635,7 @@ DEV uint3 pre_pack(const uint4 p) { return make_uint3(p.x, p.y | p.w << 31, p.z)
 
 // the epilogue's player records (lds_store_wave without the neighbourhood caches)
 DEV void trio_store_players(const TrioLds &D, const DevState &s, int ne) {
-  const int l = threadIdx.x;
+  const int l = (int)(threadIdx.x & 63);
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     const int f = j * 64 + l, e = min(f >> 2, ne - 1), q = f & 3;
@@ -3642,7 +3646,7 @@ DEV void trio_store_players(const TrioLds &D, const DevState &s, int ne) {
 
 template <int SRC>
 DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, uint32_t *__restrict__ rngs_glob) {
-  const int l = threadIdx.x;
+  const int l = (int)(threadIdx.x & 63);
   const size_t wbase = (size_t)blockIdx.x * epw;
   const DevState s = wave_view(s_glob, wbase);
   const size_t i = (size_t)l;
@@ -3827,7 +3831,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
 // duo_turn_end: the env rng is this wave's).  Which granules each record changed goes to storing
 // wave B (ring granule 3, bits 16..22).
 DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw) {
-  const int l = (int)threadIdx.x - 64;
+  const int l = (int)(threadIdx.x & 63);
   const size_t wbase = (size_t)blockIdx.x * epw;
   const DevState s = wave_view(s_glob, wbase);
   const size_t i = (size_t)l;
@@ -4059,6 +4063,8 @@ template <int SRC>
 __global__ void __launch_bounds__(256) k_env_rollout_trio(DevState s, int steps, int epw, uint32_t *__restrict__ rngs,
                                                           uint8_t *__restrict__ actions_out) {
   __shared__ TrioLds D;
+  // (roles rotated per workgroup, so that a CU's two workgroups could not put both stepping waves
+  // on one SIMD, measured the same: profiles/r04y_trio_role_rotation.txt)
   const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform
   if (threadIdx.x < 64) D.flg[threadIdx.x] = 0u;
   if (threadIdx.x < kTrioCnts) D.cnt[threadIdx.x] = 0u;
@@ -4419,8 +4425,9 @@ int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rn
     } else if (kind == RK_TRIO) {                          // selected masks, >= 3 players
       const int epw = trio_epw(s.n);
       const dim3 gt(blocks_for(s.n, epw));
-      // (k_env_fixup inside the trio launch, for shards of one workgroup per CU, was tried: no gain,
-      // its registers slowed the trio's waves, profiles/r04t_trio_fused.txt)
+      // (k_env_fixup inside the trio launch, for shards of one workgroup per CU -- inlined, or as a
+      // never-inlined call -- was slower: 20-step launch at 8,192 44.2 / 42.0 against 41.3 us,
+      // profiles/r04t_trio_fused.txt)
       hipLaunchKernelGGL((k_env_rollout_trio<MASK_SELECTED>), gt, dim3(256), 0, st, sd, steps, epw, d_rng, d_actions);
       hipLaunchKernelGGL((k_env_fixup<MASK_SELECTED>), g, dim3(64), 0, st, sd, steps, d_rng, d_actions);
     } else {
