@@ -117,3 +117,21 @@ def test_default_device_order(cg, monkeypatch):
     monkeypatch.setenv("COG_DEVICES", "0,x")
     with pytest.raises(ValueError):
         dd()
+
+
+def test_rollout_kind_selection():
+    """cog_rollout_kind (a host-only query, no device needed): the selected-mask loop with >= 3
+    players takes the trio rollout at every shard size; the stored masks and 2-player batches keep
+    round 3's kernels by size (duo <= 16,384, pipe <= 32,768, wave above: cog_engine.hip
+    rollout_kind)."""
+    if os.environ.get("COG_ROLLOUT") or os.environ.get("COG_TRIO"):
+        pytest.skip("rollout kind forced by the environment")
+    lib = ctypes.CDLL(LIB)
+    kind = lambda n, p, stored: lib.cog_rollout_kind(ctypes.c_size_t(n), p, stored)   # noqa: E731
+    TRIO, DUO, WAVE, PIPE = 3, 0, 1, 2
+    for n in (64, 4096, 8192, 16384, 32768, 53752, 65536, 131072):
+        assert kind(n, 4, 0) == TRIO and kind(n, 3, 0) == TRIO
+    for p, stored in ((2, 0), (4, 1), (3, 1)):
+        assert kind(8192, p, stored) == DUO and kind(16384, p, stored) == DUO
+        assert kind(24576, p, stored) == PIPE and kind(32768, p, stored) == PIPE
+        assert kind(65536, p, stored) == WAVE
