@@ -3549,7 +3549,7 @@ __global__ void __launch_bounds__(128) k_env_rollout_duo(DevState s, int steps, 
 //   drawing wave   records r, r + 1 (r even) once written: the plays replayed on the acting players'
 //                  decks (img: two byte updates each), then ONE turn-end pass -- a lean turn lasts at least two steps (pass
 //                  in MOVEMENT, pass in BUYING), so a player ends at most one turn in two records --
-//                  and the deck granules each record changed (ring granule 3, bits 16..22);
+//                  and the deck granules each record changed (ring granule 2, bits 16..22);
 //                  cnt[DRAW] = r + 2
 //   storing wave B record r once written: step r + 4's presampled draws (cnt[PRE] = r + 1), the
 //                  selected mask, Info, action, dones / agent_selection; on a second cursor
@@ -3829,7 +3829,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
 // each record's play replayed on the acting player's deck (the hand and active piles, as
 // Deck::activate does); then one pass over the turn ends of either record (discard + draws,
 // duo_turn_end: the env rng is this wave's).  Which granules each record changed goes to storing
-// wave B (ring granule 3, bits 16..22).
+// wave B (ring granule 2, bits 16..22).
 DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw) {
   const int l = (int)(threadIdx.x & 63);
   const size_t wbase = (size_t)blockIdx.x * epw;
