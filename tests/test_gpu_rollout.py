@@ -106,6 +106,27 @@ def test_rollout_ragged_batches_against_oracle(cg, n, chunk):
     assert np.array_equal(env.agent_selection, orc.agent_selection)
 
 
+@pytest.mark.parametrize("n,chunk,players", [(1, 7, 4), (100, 33, 3), (130, 1000, 4), (200, 20, 3)])
+def test_trio_ragged_batches_with_episode_ends(cg, n, chunk, players):
+    """The trio rollout (selected masks, >= 3 players) on batches that leave its last workgroup's
+    waves partly empty, with max_steps 30 turns so that lanes finish inside launches (parked for
+    k_env_fixup: finish, auto-reset, the rest of the launch) -- every named field against the
+    oracle."""
+    assert cg._city_of_gold.rollout_kind(n, players, False) == "trio"
+    steps = 180
+    env, smp, _ = run(cg, n, 7070 + n, players, 2, 30, steps, chunk, False)
+    orc, osm = po.OracleVec(n), po.OracleSampler(n, 7070 + n)
+    orc.reset(7070 + n, players, 3, 2, 30)
+    for _ in range(steps):
+        osm.sample(orc.selected_action_masks)
+        orc.step(osm.actions)
+    for nm in ("observations", "selected_action_masks", "infos"):
+        assert po.named_equal(getattr(env, nm), getattr(orc, nm)) is None, nm
+    assert np.array_equal(env.rewards, orc.rewards)
+    assert np.array_equal(env.dones, orc.dones)
+    assert np.array_equal(env.agent_selection, orc.agent_selection)
+
+
 def test_rollout_zero_steps_and_empty_batch(cg):
     env, smp, runner = run(cg, 64, 5, 4, 2, 100000, 0, 10, False)   # rollout(0): nothing runs
     before = env.observations.copy()
