@@ -149,3 +149,37 @@ def test_C3_selected_all_envs_vs_oracle_and_reference(cg):
     assert np.array_equal(env.hazards()[1], orc.flags()), f"{what}: hazard flags differ"
     assert assert_reference_digests(env, acts, "c3", n, 0, n, what) == 2738
     del runner, smp, env
+
+
+@pytest.mark.timeout(600)
+def test_reference_horizon_10200_steps_n8192_vs_oracle(cg):
+    """The reference benchmark's own horizon (benchmarks.py:5: 200 warm-up + 10,000 timed steps) on
+    the N=8 shard of the timed workload (8,192 envs, global 57,344..65,535, 4 players, HARD), the
+    trio rollout in 1,000-step launches: every env against the threaded C oracle after 10,200
+    steps (turn counters near 2,300: far past every test above)."""
+    import torch
+
+    import bench
+    from city_of_gold.shard import shard, shard_seed
+    lo, hi = shard(N_TOTAL, 7, 8)
+    n, base, steps = hi - lo, shard_seed(SEED, lo), 10200
+    assert cg._city_of_gold.rollout_kind(n, 4, False) == "trio"
+    env, smp, runner = bench.make(cg, n, base, 0)
+    runner.set_chunk(1000)
+    runner.rollout(steps)
+    runner.sync()
+    env.sync_host()
+    acts = torch.from_dlpack(smp.dlpack()).cpu().numpy().view(po.ACTION).reshape(n)
+    orc, osm = po.OracleVec(n), po.OracleSampler(n, base)
+    orc.reset_threaded(base, 4, 3, 2, 100000)
+    po.run_threaded(orc, osm, steps, po.host_threads())
+    what = f"{n} envs (global {lo}..{hi - 1}), {steps} steps"
+    for nm in FIELDS:
+        bad = first_bad_env(getattr(env, nm), getattr(orc, nm))
+        assert bad is None, f"{what}: {nm}.{bad[1]} of env {bad[0]} differs from the oracle"
+    bad = first_bad_env(acts, osm.actions)
+    assert bad is None, f"{what}: sampled action {bad[1]} of env {bad[0]} differs"
+    for nm in ("rewards", "dones", "agent_selection"):
+        assert np.array_equal(getattr(env, nm), getattr(orc, nm)), f"{what}: {nm} differs"
+    assert np.array_equal(env.hazards()[1], orc.flags()), f"{what}: hazard flags differ"
+    del runner, smp, env
