@@ -152,16 +152,17 @@ def test_C3_selected_all_envs_vs_oracle_and_reference(cg):
 
 
 @pytest.mark.timeout(600)
-def test_reference_horizon_10200_steps_n8192_vs_oracle(cg):
+@pytest.mark.parametrize("world,rank", [(8, 7), (1, 0)], ids=["n8192_N8_rank7", "n65536_N1"])
+def test_reference_horizon_10200_steps_vs_oracle(cg, world, rank):
     """The reference benchmark's own horizon (benchmarks.py:5: 200 warm-up + 10,000 timed steps) on
-    the N=8 shard of the timed workload (8,192 envs, global 57,344..65,535, 4 players, HARD), the
-    trio rollout in 1,000-step launches: every env against the threaded C oracle after 10,200
-    steps (turn counters near 2,300: far past every test above)."""
+    the N=8 shard (8,192 envs, global 57,344..65,535) and on the whole N=1 batch (65,536 envs) of
+    the timed workload (4 players, HARD), the trio rollout in 1,000-step launches: every env
+    against the threaded C oracle after 10,200 steps (far past every test above)."""
     import torch
 
     import bench
     from city_of_gold.shard import shard, shard_seed
-    lo, hi = shard(N_TOTAL, 7, 8)
+    lo, hi = shard(N_TOTAL, rank, world)
     n, base, steps = hi - lo, shard_seed(SEED, lo), 10200
     assert cg._city_of_gold.rollout_kind(n, 4, False) == "trio"
     env, smp, runner = bench.make(cg, n, base, 0)
