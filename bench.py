@@ -18,10 +18,11 @@ the bytes a one-launch-per-step run leaves (tests/test_gpu_rollout.py).  No host
 max/sum of scalars (gloo).
 
 Also reported (rank 0; the extra lines only at N=1, so a scaling run stays short):
-  roofline       the dominant kernel (the trio rollout) against HBM by SURVEY 8d's 800 B/env-step
-                 (roofline() below), with the counter-measured HBM traffic of the same launch shape
-                 (FETCH x 2 + WRITE, gfx950 corrections), round 3's L2 store model as a record and
-                 `valu_issue` the VALU rate against the SIMDs' peak.
+  roofline       the dominant kernel (the trio rollout) against HBM by the bytes it moves (PMC
+                 counters of the same launch shape: FETCH x 2 + WRITE, gfx950 corrections), the
+                 limiter that applies (the stepping wave's instruction stream, busy fraction from
+                 phase stamps), SURVEY 8d's 800 B/env-step as a labelled equivalent, round 3's L2
+                 store model as a record and `valu_issue` the VALU rate against the SIMDs' peak.
   shard_sizes    rollout us/step at the N=1 batch (65,536 on one GPU) and the N=8 shard (8,192)
   per_launch     one kernel launch per step (k_env_step<selected>)
   host_loop      the reference's numpy loop through the host API at C2 (256, EASY) and the C4
@@ -344,26 +345,38 @@ KERNEL_LABEL = {"wave": "k_env_rollout<selected>", "pipe": "k_env_rollout_pipe<s
                 "trio": "k_env_rollout_trio<selected> + k_env_fixup<selected>"}
 
 
-def roofline(prof, n, k_chunk, launch_s, kind="trio"):
+def roofline(prof, n, k_chunk, launch_s, kind="trio", stamps=None):
     """The dominant kernel -- the persistent rollout that runs a shard of n envs (`kind`: trio, wave,
-    pipe or duo, cog_rollout_kind) -- against HBM, SURVEY 8d's way: achieved = 800 algorithmic bytes
-    per env-step (the bytes a one-launch-per-step sample + step would move) x the launch's
-    env-steps / the launch time (HIP events), peak = 8 TB/s.  The rollout keeps every env's state on
-    chip between steps, so it moves far fewer bytes than that and frac can exceed 1; `traffic` is
-    what it does move, the HBM bytes of a rocprofv3 --pmc pass of this exact engine source AT THIS
-    LAUNCH SHAPE (n envs, k steps per launch, same kernel: profiles/pmc_profile.json `rollouts`;
-    FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 corrections), with counter_frac = traffic / time / peak.
-    store_model: round 3's L2 store-cost model of the same launch (hits x c_hit + misses x c_miss,
-    tools/storeprobe.hip); the trio beats it (frac > 1), so it is no bound -- kept as a record.  No
-    profile of this shape: traffic and store_model are null."""
+    pipe or duo, cog_rollout_kind) -- against HBM, by the bytes it really moves: `traffic` is the HBM
+    bytes of one launch of this exact engine source AT THIS LAUNCH SHAPE (n envs, k steps per launch,
+    same kernel) from a rocprofv3 --pmc pass (profiles/pmc_profile.json `rollouts`: FETCH_SIZE x 2 +
+    WRITE_SIZE, the gfx950 corrections of MI355X_MICROARCH.md), achieved = traffic / the launch time
+    (HIP events on the runner's stream, live), peak = 8 TB/s, frac = achieved / peak -- reproducible
+    from pmc_profile.json and the rocprofv3 kernel trace of the same command.
+
+    The HBM roofline is not what limits this kernel (frac ~0.4): `limiter` names the bound that
+    applies, the stepping wave's dependent instruction stream, with its busy fraction
+    from the s_memtime phase stamps of a diagnostic build of the same source (profiles/
+    stamps_profile.json: the share of a step the stepping wave spends issuing its own step rather
+    than waiting for the other waves' progress counters) when one matches this engine.
+    `survey_8d_equivalent` is SURVEY 8d's 800 algorithmic bytes per env-step over the same time: the
+    bytes a one-launch-per-step sample + step would move; the rollout keeps each env's state on chip
+    between steps, so that figure exceeds the HBM peak and is no roofline.  store_model: round 3's L2
+    store-cost model of the same launch (a record).  No profile of this engine at this shape:
+    traffic, achieved and frac are null."""
     alg = STEP_BYTES * n * k_chunk
     out = {"bound": "hbm", "kernel": KERNEL_LABEL.get(kind, kind), "rollout_kind": kind, "unit": "GB/s",
-           "achieved": alg / launch_s / 1e9, "peak": HBM_PEAK_GBS, "frac": alg / launch_s / 1e9 / HBM_PEAK_GBS,
-           "traffic": None, "algorithmic_bytes_per_launch": alg, "env_steps_per_s": n * k_chunk / launch_s,
-           "kernel_ms": launch_s * 1e3, "steps_per_launch": k_chunk, "envs_per_launch": n, "store_model": None,
-           "note": "achieved / frac use SURVEY 8d's 800 B per env-step; the rollout keeps the state on chip, "
-                   "so its real HBM bytes are `traffic` (counter_frac); it is bound by the stepping wave's "
-                   "instruction latency (DESIGN.md 6)"}
+           "achieved": None, "peak": HBM_PEAK_GBS, "frac": None, "traffic": None,
+           "env_steps_per_s": n * k_chunk / launch_s, "kernel_ms": launch_s * 1e3, "steps_per_launch": k_chunk,
+           "envs_per_launch": n,
+           "survey_8d_equivalent": {"bytes_per_env_step": STEP_BYTES, "bytes_per_launch": alg,
+                                    "GBs": alg / launch_s / 1e9, "x_peak": alg / launch_s / 1e9 / HBM_PEAK_GBS,
+                                    "note": "SURVEY 8d's algorithmic bytes of a one-launch-per-step sample + step; "
+                                            "the rollout keeps the state on chip, so this is no roofline"},
+           "limiter": {"kind": "issue: the stepping wave's dependent instruction stream (DESIGN.md 6)"},
+           "store_model": None,
+           "note": "achieved / frac: the HBM bytes this launch moves (PMC counters of this engine source at this "
+                   "launch shape) / the live launch time; the kernel is limited by the stepping wave (limiter)"}
     waves = (n + 63) // 64
     valu_peak = N_SIMD * CLOCK_HZ / VALU_CYC                # wave64 VALU instructions per second
     e = ((prof or {}).get("rollouts") or {}).get("%d:%d" % (n, k_chunk))
@@ -385,9 +398,15 @@ def roofline(prof, n, k_chunk, launch_s, kind="trio"):
     if e and e.get("bytes_per_launch") is not None:
         tr = e["bytes_per_launch"] + ((e.get("companion") or {}).get("bytes_per_launch") or 0.0)
         out["traffic"] = tr
-        out["counter_GBs"] = tr / launch_s / 1e9
-        out["counter_frac"] = tr / launch_s / 1e9 / HBM_PEAK_GBS
+        out["achieved"] = tr / launch_s / 1e9
+        out["frac"] = tr / launch_s / 1e9 / HBM_PEAK_GBS
         out["counter_bytes_per_env_step"] = tr / n / k_chunk
+        out["pmc_kernel_ns"] = e.get("kernel_ns")
+    st = ((stamps or {}).get("shapes") or {}).get(str(n))
+    if st:
+        out["limiter"].update({k: st[k] for k in ("busy_ticks_per_step", "wait_ticks_per_step", "ticks_per_step",
+                                                  "busy_frac", "steps_per_launch") if k in st})
+        out["limiter"]["source"] = "profiles/stamps_profile.json (tools/duoprobe.cpp -DCOG_STAMPS, same engine source)"
     pw = (e or {}).get("per_wave_step") or {}
     if pw.get("valu"):
         achieved = pw["valu"] * waves * k_chunk / launch_s
@@ -397,9 +416,20 @@ def roofline(prof, n, k_chunk, launch_s, kind="trio"):
             "issue_quads_per_wave_step": pw.get("active_inst_any"), "wait_quads_per_wave_step": pw.get("wait_any"),
             "wave_quads_per_wave_step": pw.get("wave_cycles"),
             "note": "peak = 1,024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU; per 64-env wave and step (the duo / trio / "
-                    "pipe: every wave of the workgroup); not the bound: the stepping wave's dependent "
-                    "instruction latency sets the step"}
+                    "pipe: every wave of the workgroup); chip-wide, not the critical path (limiter)"}
     return out
+
+
+def load_stamps():
+    """profiles/stamps_profile.json when it was measured on this exact engine source; else None."""
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from pmc_profile import engine_hash
+        with open(os.path.join(ROOT, "profiles", "stamps_profile.json")) as f:
+            p = json.load(f)
+        return p if p.get("engine_sha") == engine_hash() else None
+    except Exception:
+        return None
 
 
 def main():
@@ -454,7 +484,7 @@ def main():
     k_chunk = min(chunk, args.steps)
     launch_s = kernel_time(runner, k_chunk, max(3, min(20, 4000 // max(k_chunk, 1))))
     prof = load_profile()
-    roof = roofline(prof, n, k_chunk, launch_s, cg._city_of_gold.rollout_kind(n, N_PLAYERS, False))
+    roof = roofline(prof, n, k_chunk, launch_s, cg._city_of_gold.rollout_kind(n, N_PLAYERS, False), load_stamps())
 
     haz, per = env.hazards()
     n_erase = int(((per & HAZ_ERASE_PAST) != 0).sum())

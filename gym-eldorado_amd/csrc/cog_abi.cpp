@@ -280,6 +280,7 @@ struct EnvShard {
   // (launch_step_pub), and pub_done tells finish() that the step already did.
   bool host_synced = false, pub_done = false;
   Signal done;                        // completion word: word 32 of the shard's error line
+  uint32_t park_seq = 0;              // rollout launches with a fix-up so far (DevState::park_par)
 };
 
 struct cog_env {
@@ -335,9 +336,11 @@ bool single(const cog_env *e) { return e->sh.size() == 1; }
 
 // Envs with host views, for cog_sampler_sample: when the masks it gets are one env shard's own
 // pinned selected-mask view on the sampler shard's device, and that shard's views equal HBM
-// (host_synced: its last call published and completed), the sampler reads the same records in
-// HBM instead of over PCIe.  The views are the env's outputs -- the engine
-// never reads them back, its step included -- so a caller's writes into them go unseen either way.
+// (host_synced: its last publish stored them), the sampler reads the same records in HBM instead
+// of over PCIe.  The views are the env's outputs, handed to Python read-only
+// (pybind_module.cpp readonly()), so the bytes in HBM are the bytes of the view.  A step may still
+// be in flight on the env's stream (an asynchronous runner.step() publishes itself and keeps
+// host_synced): the caller then orders the sampler's stream after it (env_stream_in_flight).
 std::mutex g_host_envs_mu;
 std::vector<cog_env *> g_host_envs;
 
@@ -348,14 +351,17 @@ void host_env_register(cog_env *e, bool on) {
   if (!on && it != g_host_envs.end()) g_host_envs.erase(it);
 }
 
-const uint8_t *env_masks_in_hbm(const cog_action_mask_t *masks, size_t n, int device) {
+EnvShard *env_masks_in_hbm(const cog_action_mask_t *masks, size_t n, int device) {
   if (std::getenv("COG_NO_HBM_MASKS")) return nullptr;    // (A/B)
   std::lock_guard<std::mutex> lk(g_host_envs_mu);
   for (cog_env *e : g_host_envs)
-    for (const EnvShard &k : e->sh)
-      if (e->h_sel + k.first == masks && k.n == n && k.device == device && k.host_synced) return k.s.sel;
+    for (EnvShard &k : e->sh)
+      if (e->h_sel + k.first == masks && k.n == n && k.device == device && k.host_synced) return &k;
   return nullptr;
 }
+// work of the env shard that may still be running on its stream: a step that publishes itself and
+// whose completion no sync has consumed yet (pub_done), or any queued completion word
+bool env_stream_in_flight(const EnvShard &k) { return k.pub_done || k.done.queued; }
 
 void env_free(cog_env *e) {
   if (!e) return;
@@ -364,7 +370,7 @@ void env_free(cog_env *e) {
     DeviceGuard g(k.device);
     if (k.stream) (void)hipStreamSynchronize(k.stream);
     void *dev[] = {k.s.obs, k.outs, k.s.priv, k.s.grid, k.s.cgrid, k.s.heads, k.s.gen, k.s.dirty, k.d_actions, k.mir,
-                   k.s.park, k.done.ctr};
+                   k.s.park, k.s.parkq, k.done.ctr};
     for (void *p : dev)
       if (p) (void)hipFree(p);
     zc_free(k.h_outs);
@@ -611,6 +617,7 @@ int env_shard_init(EnvShard &k, uint32_t default_seed, uint32_t *err_word) {
       (rc = dmalloc(&s.cgrid, n * (size_t)COG_CELLS)) || (rc = dmalloc(&s.heads, n * 5 * sizeof(uint4))) ||
       (rc = dmalloc(&s.gen, n * sizeof(cog::GenScratch))) || (rc = dmalloc(&s.dirty, n * sizeof(uint32_t))) ||
       (rc = dmalloc(&k.d_actions, n * COG_ACTION_BYTES)) || (rc = dmalloc(&s.park, n * sizeof(uint32_t))) ||
+      (rc = dmalloc(&s.parkq, cog::park_list_bytes(n))) ||
       (rc = dmalloc(&k.done.ctr, 256)) || (rc = zc_alloc(&k.h_outs, L.alloc)))
     return rc;
   std::memset(k.h_outs, 0, L.alloc);
@@ -635,6 +642,7 @@ int env_shard_init(EnvShard &k, uint32_t default_seed, uint32_t *err_word) {
   for (auto &zz : z)
     if (zz.b) HIPCHK(hipMemsetAsync(zz.p, 0, zz.b, k.stream));
   if (n) HIPCHK(hipMemsetAsync(s.park, 0xff, n * sizeof(uint32_t), k.stream));   // no env parked
+  HIPCHK(hipMemsetAsync(s.parkq, 0, cog::park_list_bytes(n), k.stream));          // both counters 0
   if (cog::launch_init(s, nullptr, default_seed, k.stream))
     return fail(COG_ERR_HIP, std::string("env init kernel failed: ") + hipGetErrorString(hipGetLastError()));
   return COG_OK;
@@ -1159,7 +1167,14 @@ int cog_sampler_sample(cog_sampler *s, const cog_action_mask_t *masks, size_t n)
   for (SamplerShard &k : s->sh) {
     if (!k.n) continue;
     DeviceGuard g(k.device);
-    const uint8_t *dm = env_masks_in_hbm(masks + k.first, k.n, k.device);   // an env's own view: HBM
+    const uint8_t *dm = nullptr;
+    if (EnvShard *ek = env_masks_in_hbm(masks + k.first, k.n, k.device)) {    // an env's own view: HBM
+      if (env_stream_in_flight(*ek)) {                     // the sampler's stream after the env's step
+        HIPCHK(hipEventRecord(ek->ev, ek->stream));
+        HIPCHK(hipStreamWaitEvent(k.stream, ek->ev, 0));
+      }
+      dm = ek->s.sel;
+    }
     if (!dm) {
       dm = zc_device(masks + k.first, k.n * COG_MASK_BYTES);                // else read in place when pinned
       if (!dm || !zc_same_on(k.device, masks + k.first)) {
@@ -1294,7 +1309,7 @@ static int runner_launch_fused(cog_runner *r, int steps) {
     if (r->chunk > 1) {                                    // persistent kernels, chunk steps each
       for (int t = 0; t < steps; t += r->chunk)
         if (cog::launch_rollout(s, src, std::min(r->chunk, steps - t), q.d_rng, q.d_actions, k.stream,
-                                r->env->n_players >= 3))
+                                r->env->n_players >= 3, &k.park_seq))
           return fail(COG_ERR_HIP, std::string("rollout launch failed: ") + hipGetErrorString(hipGetLastError()));
     } else {
       for (int t = 0; t < steps; t++)

@@ -106,6 +106,12 @@ struct DevState {
   unsigned long long *stamps;        // diagnostic builds (COG_STAMPS) only: per-wave phase clocks
   uint32_t *park;                    // [n] rollout park codes: the step at which an env's episode
                                      // ended inside a launch (~0u: none), read by the fix-up kernel
+  // the parked workgroups of a duo / trio launch, for k_env_fixup: [0], [1] two counters used by
+  // alternate launches (park_par, the host's count of such launches mod 2: a launch appends to
+  // counter park_par and zeroes the other one, which the previous launch's fix-up has read), then
+  // the list of workgroup indices with a parked env (park_list_bytes(n))
+  uint32_t *parkq;
+  uint32_t park_par;
   // direct publish (launch_step_pub only; null otherwise): device addresses of the shard's pinned
   // ObsData view and outs block, and the publish mirror (k_publish's `mir`)
   uint8_t *pub_obs, *pub_outs, *pub_mir;
@@ -159,11 +165,14 @@ bool publish_can_signal(size_t n, size_t outs_bytes, bool actions);
 int launch_sample_step(const DevState &s, int mask_source, uint32_t *d_rng, uint8_t *d_actions,
                        void *stream);
 // persistent K-step runner loop; defer_ok: every env of the shard has >= 3 players (the trio
-// rollout's deferred turn end may run on shards of <= 16,384 envs with the selected masks)
+// rollout's deferred turn end then runs the selected-mask loop at every shard size)
+// park_seq: the shard's count of launches with a fix-up (counts them; alternate launches use
+// alternate counters of DevState::parkq)
 int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions,
-                   void *stream, bool defer_ok = false);
-int rollout_kind_of(size_t n, int mask_source, bool defer_ok);
-int trio_epw(size_t n);                                          // envs per trio workgroup (32 or 64)   // 0 duo, 1 wave, 2 pipe, 3 trio (launch_rollout)
+                   void *stream, bool defer_ok, uint32_t *park_seq);
+inline size_t park_list_bytes(size_t n) { return (2 + (n + 31) / 32) * sizeof(uint32_t); }
+int rollout_kind_of(size_t n, int mask_source, bool defer_ok);   // 0 duo, 1 wave, 2 pipe, 3 trio
+int trio_epw(size_t n);                                          // envs per trio workgroup (32 or 64)
 int launch_seed_sampler(size_t n, uint64_t seed, size_t first, uint32_t *d_rng, void *stream);
 // completion word: stores seq into *d_word (device address of a pinned host word) once every
 // earlier packet of the stream has completed

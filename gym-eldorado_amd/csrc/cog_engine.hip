@@ -21,6 +21,7 @@
 //                    (runner.h:46-55)
 //   k_sync_heads     mask bit-vectors of every env from its byte records (init / reset)
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -2797,8 +2798,8 @@ DEV void lds_players(const LaneLds &L, int l, int ag, int na, Snap &S) {
 // out of its allocation.  A wave with nothing parked ends after the lean pass (round 1 launched
 // the fix-up as a second kernel: 4.8 us per launch even when it had nothing to do).
 // park codes: bits 0..29 the step t; kParkFinish: step t finished the episode (else the env
-// started step t done); kParkRedo: step t was not run (the duo rollout's deferred turn end met an
-// action that draws from the env rng, duo_stepper) -- the fix-up runs it with the full step
+// started step t done); kParkRedo: step t was not run (the trio's stepping wave met an action
+// outside its lean step, lean_ok in trio_stepper) -- the fix-up runs it with the full step
 constexpr uint32_t kParkNone = ~0u, kParkFinish = 1u << 31, kParkRedo = 1u << 30;
 constexpr uint32_t kParkStep = kParkRedo - 1u;
 // The records of a wave's envs seen from the wave's first env: a per-wave (scalar) base and a
@@ -2822,6 +2823,19 @@ DEV DevState wave_view(const DevState &s, size_t base) {
   v.first += base;
   v.n = s.n > base ? s.n - base : 0;
   return v;
+}
+// a duo / trio workgroup with a parked env appends its index to the launch's parked list (one
+// atomic per such wave), so that k_env_fixup visits only those (DevState::parkq)
+DEV void park_list_push(const DevState &s_glob, bool parked) {
+  if (__builtin_amdgcn_ballot_w64(parked) && (threadIdx.x & 63) == 0) {
+    const uint32_t j = atomicAdd(&s_glob.parkq[s_glob.park_par], 1u);
+    s_glob.parkq[2 + j] = blockIdx.x;
+  }
+}
+// the other counter back to 0 for the next launch (the previous launch's fix-up, which read it,
+// has completed: same stream)
+DEV void park_list_clear_other(const DevState &s_glob) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) s_glob.parkq[s_glob.park_par ^ 1u] = 0u;
 }
 // Two-wave rollout for small shards (k_env_rollout_pipe): the stepping wave hands each step's
 // outputs to a second wave of its workgroup through a double-buffered LDS ring, and the second
@@ -2917,11 +2931,13 @@ DEV void out_record_store(const OutRing &O, int b, int l, const DevState &s, siz
   reinterpret_cast<uint2 *>(actions_out + i * COG_ACTION_BYTES)[0] = make_uint2(o2.y, o2.z);
 }
 
+// wbase_in: the wave's first env (k_env_fixup: a parked workgroup's); default blockIdx.x * NL
 template <int SRC, bool FIX, int NL, bool PIPE = false>
 DEV uint32_t rollout_pass(LaneLds<NL> &L, const DevState &s_glob, int steps, uint32_t *__restrict__ rngs_glob,
-                          uint8_t *__restrict__ actions_glob, uint32_t park, OutRing *O = nullptr) {
+                          uint8_t *__restrict__ actions_glob, uint32_t park, OutRing *O = nullptr,
+                          size_t wbase_in = ~(size_t)0) {
   const int l = threadIdx.x;                               // (the stepping wave: threads 0..NL-1)
-  const size_t wbase = (size_t)blockIdx.x * NL;
+  const size_t wbase = wbase_in != ~(size_t)0 ? wbase_in : (size_t)blockIdx.x * NL;
   const size_t i0 = wbase + l;
   // (s, i): the wave's view and the lane's index in it, for every record access; the wave's
   // generation, its encode and the regenerated-map list take the shard's (s_glob, i_glob)
@@ -3221,26 +3237,8 @@ DEV void duo_store_env_private(const DevState &s, size_t i, const RegEnv &R) {
 // then the saved mask gains the drawn cards (draw's mask updates, cards.cpp:183-211, precede
 // save_actionmask).  Nothing the stepping wave reads before that player acts again depends on it:
 // with >= 3 players the next two agents are other players, whose turn ends lie at least two steps
-// back.  An action that would draw from the env rng inside a step (step_draws_rng: never taken in
-// the canonical loop) parks the env with kParkRedo, and k_env_fixup runs that step and
-// the rest with the full step.
-// DEFER: whether step_regs would draw from the env rng for this action -- a special that draws
-// cards (cards.cpp:8-36) or a move whose requirement discards / removes random active cards
-// (player.cpp:85-131) -- the same dispatch as step_regs (environment.cpp:104-160)
-DEV bool step_draws_rng(const RegEnv &R, const uint8_t act[5]) {
-  if (act[0]) return false;                                // play_card
-  if (act[1]) {
-    const uint32_t sp = cardf(kSpecial, act[1] - 1);
-    return sp == COG_SPECIAL_DRAW2 || sp == COG_SPECIAL_DRAW3 || sp == COG_SPECIAL_DRAW1_REMOVE1 ||
-           sp == COG_SPECIAL_DRAW2_REMOVE2;
-  }
-  if (act[3] && !R.P.next_move_free) {
-    const uint64_t v = (uint64_t)R.cells_a.x | (uint64_t)R.cells_a.y << 32;
-    const uint32_t req = COG_HEX_REQ((uint32_t)(v >> (8 * act[3])) & 0xffu);
-    return req == COG_REQ_REMOVE || req == COG_REQ_DISCARD;
-  }
-  return false;
-}
+// back.  Any action outside the lean step (lean_ok: never in the canonical loop) parks
+// the env with kParkRedo, and k_env_fixup runs that step and the rest with the full step.
 
 template <int SRC>
 DEV void duo_stepper(DuoLds &D, const DevState &s_glob, int steps, uint32_t *__restrict__ rngs_glob) {
@@ -3358,6 +3356,7 @@ DEV void duo_stepper(DuoLds &D, const DevState &s_glob, int steps, uint32_t *__r
     rngs[i] = srng;
   }
   if (l < ne) s.park[i] = park;
+  park_list_push(s_glob, park != kParkNone);
   lds_store_wave<DuoLds, 64>(D, s, 0, ne);                 // every player's records (cooperative)
 }
 
@@ -3513,6 +3512,7 @@ __global__ void __launch_bounds__(128) k_env_rollout_duo(DevState s, int steps, 
   // (roles rotated per workgroup, so that a CU's two workgroups could not put both stepping waves
   // on one SIMD, measured the same: profiles/r04y_trio_role_rotation.txt)
   const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform
+  park_list_clear_other(s);
   uid_tab_fill(D.tab);
   if (role == 0) {
 #ifndef DUO_NOPRIO                                         // (diagnostic A/B builds only)
@@ -3525,7 +3525,7 @@ __global__ void __launch_bounds__(128) k_env_rollout_duo(DevState s, int steps, 
 }
 
 // ------------------------------------------------------------------------------------------
-// Trio rollout (round 4): the selected-mask loop with >= 3 players on shards of <= 32,768 envs,
+// Trio rollout (round 4): the selected-mask loop with >= 3 players at every shard size (cog_rollout_kind),
 // one step's work spread over four waves per 64 envs.  The stepping wave runs the lean step
 // (step_lean: sample, play or pass, turn change, done check) and nothing else; the drawing wave
 // owns the decks (replays each play on its copy, runs the turn ends' discard + draws with the env
@@ -3577,7 +3577,10 @@ constexpr int kTrioRingG = 3;
 constexpr int kTrioDepth = COG_TRIO_DEPTH;                 // ring slots (records in flight)
 constexpr int kTrioLead = 4;                               // presampled draws: steps ahead of the record
 constexpr int kTrioBLag = 2;                               // storing wave B: deck cursor behind its front
-enum TrioCnt : int { CNT_REC = 0, CNT_DRAW, CNT_STA, CNT_STB, CNT_PRE, CNT_FIN, kTrioCnts };
+// CNT_ABORT: set (sticky) by the first progress wait that times out; every later wait of every
+// wave returns at once, so a broken invariant ends the launch promptly with the error set
+// (instead of one ~0.2 s timeout per remaining wait)
+enum TrioCnt : int { CNT_REC = 0, CNT_DRAW, CNT_STA, CNT_STB, CNT_PRE, CNT_FIN, CNT_ABORT, kTrioCnts };
 constexpr uint32_t kTrioSpinLimit = 1u << 21;             // polls (~0.2 s)
 struct TrioLds {
   uint4 img[4][7][64];                // every player's DeckObs (the drawing wave's)
@@ -3597,7 +3600,7 @@ static_assert((kTrioDepth & (kTrioDepth - 1)) == 0 && kTrioDepth >= 4, "ring slo
 // in one round trip -- only when the one it needs is short: the counters only grow, and what an
 // acquire read once made visible stays so.  A waiting wave sleeps between reads.
 struct TrioCnt6 {
-  uint32_t rec = 0, draw = 0, sta = 0, stb = 0, pre = 0, fin = 0;
+  uint32_t rec = 0, draw = 0, sta = 0, stb = 0, pre = 0, fin = 0, abort = 0;
 };
 DEV void cnt_read(const TrioLds &D, TrioCnt6 &c) {
   uint32_t v[kTrioCnts];
@@ -3610,22 +3613,29 @@ DEV void cnt_read(const TrioLds &D, TrioCnt6 &c) {
   c.stb = __builtin_amdgcn_readfirstlane(v[CNT_STB]);
   c.pre = __builtin_amdgcn_readfirstlane(v[CNT_PRE]);
   c.fin = __builtin_amdgcn_readfirstlane(v[CNT_FIN]);
+  c.abort = __builtin_amdgcn_readfirstlane(v[CNT_ABORT]);
 }
-DEV void cnt_store(TrioLds &D, int k, uint32_t v) {        // publishes this wave's earlier LDS writes
+// Publishes this wave's earlier LDS writes, all lanes' included, through lane 0's release store.
+// That relies on the wave executing as one: the release's s_waitcnt lgkmcnt(0) is issued by the
+// wave and covers every lane's outstanding LDS writes (LDS ops of a wave complete in order), which
+// the AMDGPU backend guarantees for a wave's own ops, though the HIP memory model speaks of threads.
+DEV void cnt_store(TrioLds &D, int k, uint32_t v) {
   if ((threadIdx.x & 63) == 0) __hip_atomic_store(&D.cnt[k], v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 // wait (wave-uniform) until counter `field` of c (a member of c) >= v
-DEV void cnt_wait(const TrioLds &D, TrioCnt6 &c, const uint32_t &field, uint32_t v, const DevState &s) {
-  if (field >= v) return;
+DEV void cnt_wait(TrioLds &D, TrioCnt6 &c, const uint32_t &field, uint32_t v, const DevState &s) {
+  if (field >= v || c.abort) return;
   for (uint32_t spins = 0;; spins++) {
     cnt_read(D, c);
-    if (field >= v) return;
+    if (field >= v || c.abort) return;
     if (spins >= kTrioSpinLimit) {
       if ((threadIdx.x & 63) == 0) {
         atomicOr(&s.status[0], F_SYNC_TIMEOUT);
         atomicAdd(&s.status[1], 1u);
         *s.err = 1u;
+        __hip_atomic_store(&D.cnt[CNT_ABORT], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
+      c.abort = 1u;
       return;
     }
     __builtin_amdgcn_s_sleep(2);
@@ -3822,6 +3832,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     reinterpret_cast<uint32_t *>(s.priv + i)[7] = R.flags | fl;
   }
   if (l < ne) s.park[i] = park;
+  park_list_push(s_glob, park != kParkNone);
   trio_store_players(D, s, ne);                            // every player's records (cooperative)
 }
 
@@ -4068,6 +4079,7 @@ __global__ void __launch_bounds__(256) k_env_rollout_trio(DevState s, int steps,
   const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform
   if (threadIdx.x < 64) D.flg[threadIdx.x] = 0u;
   if (threadIdx.x < kTrioCnts) D.cnt[threadIdx.x] = 0u;
+  park_list_clear_other(s);
   uid_tab_fill(D.tab);                                     // (ends on a barrier)
   if (role == 0) {
     __builtin_amdgcn_s_setprio(3);
@@ -4083,31 +4095,37 @@ __global__ void __launch_bounds__(256) k_env_rollout_trio(DevState s, int steps,
   if (l == 0) __hip_atomic_fetch_add(&D.cnt[CNT_FIN], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// The episode ends k_env_rollout_duo parked: a wave with a parked lane runs k_env_rollout's
-// fix-up pass for exactly those lanes (finish_episode, dones, auto-reset with the wave's map
-// generation and encode, then the env's remaining steps with the full step); a wave with none
-// returns after one load.  Same stream, right after the rollout launch: nothing reads the envs
-// in between.
+// The envs a duo / trio launch parked (episode ends; the trio's actions outside its lean step):
+// for each workgroup on the launch's parked list (park_list_push), one wave runs k_env_rollout's
+// fix-up pass for exactly the parked lanes (finish_episode, dones, auto-reset with the wave's map
+// generation and encode, then the env's remaining steps with the full step).  A small grid strides
+// over the list; with nothing parked every wave returns after one scalar load (round 4 dispatched
+// one wave per 64 envs, each reading its envs' park codes: 4.1-4.7 us per launch at 65,536 envs).
+// Same stream, right after the rollout launch: nothing reads the envs in between.  epw: envs per
+// workgroup of the launch (64, or the trio's 32); lanes epw.. idle.
 template <int SRC>
 __global__ void __launch_bounds__(64) k_env_fixup(DevState s, int steps, uint32_t *__restrict__ rngs,
-                                                  uint8_t *__restrict__ actions_out) {
+                                                  uint8_t *__restrict__ actions_out, int epw) {
   __shared__ LaneLds<64> L;
-  const size_t base = (size_t)blockIdx.x * 64;
-  const size_t i0 = base + threadIdx.x;
-  const uint32_t park = i0 < s.n ? s.park[i0] : kParkNone;
-  if (!__builtin_amdgcn_ballot_w64(park != kParkNone)) return;   // (wave-uniform)
+  const uint32_t cnt = s.parkq[s.park_par];                // (uniform: a scalar load)
+  if (blockIdx.x >= cnt) return;
   uid_tab_fill(L.tab);
-  rollout_pass<SRC, true, 64>(L, s, steps, rngs, actions_out, park);
-  if (park != kParkNone) {                                 // the parked envs' player records
-    const int l = (int)threadIdx.x;
-    uint4 *pw = reinterpret_cast<uint4 *>(s.priv + i0);
+  for (uint32_t w = blockIdx.x; w < cnt; w += gridDim.x) {
+    const size_t base = (size_t)s.parkq[2 + w] * (size_t)epw;
+    const size_t i0 = base + threadIdx.x;
+    const uint32_t park = (int)threadIdx.x < epw && i0 < s.n ? s.park[i0] : kParkNone;
+    rollout_pass<SRC, true, 64>(L, s, steps, rngs, actions_out, park, nullptr, base);
+    if (park != kParkNone) {                               // the parked envs' player records
+      const int l = (int)threadIdx.x;
+      uint4 *pw = reinterpret_cast<uint4 *>(s.priv + i0);
 #pragma unroll
-    for (int p = 0; p < 4; p++) {
-      pw[4 + p] = L.pl[p][l];
-      reinterpret_cast<uint2 *>(pw + 8)[p] = L.cells[p][l];
-      s.heads[5 * i0 + 1 + p] = L.heads[p][l];
+      for (int p = 0; p < 4; p++) {
+        pw[4 + p] = L.pl[p][l];
+        reinterpret_cast<uint2 *>(pw + 8)[p] = L.cells[p][l];
+        s.heads[5 * i0 + 1 + p] = L.heads[p][l];
+      }
+      s.park[i0] = kParkNone;
     }
-    s.park[i0] = kParkNone;
   }
 }
 
@@ -4406,33 +4424,46 @@ int trio_epw(size_t n) {
   (void)n;
   return 64;
 }
+// k_env_fixup's grid: at most this many one-wave workgroups stride over the parked list
+// ($COG_FIXUP_GRID overrides; A/B only).  A wave per CU keeps a launch with every workgroup parked
+// (short episodes) running in parallel, and a launch with none parked cheap.
+static unsigned fixup_grid(unsigned nblocks) {
+  static const unsigned cap = [] {
+    const char *e = getenv("COG_FIXUP_GRID");
+    const int v = e && *e ? atoi(e) : 0;
+    return v > 0 ? (unsigned)v : 256u;
+  }();
+  return std::max(1u, std::min(nblocks, cap));
+}
 int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions, void *stream,
-                   bool defer_ok) {
+                   bool defer_ok, uint32_t *park_seq) {
   if (!s.n || steps <= 0) return 0;
   const int kind = rollout_kind(s.n, mask_source, defer_ok);
   if (kind == RK_DUO || kind == RK_TRIO) {
+    if (!park_seq || !s.parkq) return -1;
     const hipStream_t st = (hipStream_t)stream;
-    const dim3 g(blocks_for(s.n, 64));
     static const int redo_at = [] {                        // test hook (DevState::redo_at)
       const char *e = getenv("COG_DEBUG_REDO_STEP");
       return e && *e ? atoi(e) : -1;
     }();
     DevState sd = s;
     sd.redo_at = redo_at;
+    sd.park_par = (*park_seq)++ & 1u;
+    const int epw = kind == RK_TRIO ? trio_epw(s.n) : 64;
+    const unsigned nb = blocks_for(s.n, epw);
+    const dim3 g(nb), gf(fixup_grid(nb));
     if (mask_source == MASK_STORED) {
       hipLaunchKernelGGL((k_env_rollout_duo<MASK_STORED>), g, dim3(128), 0, st, sd, steps, d_rng, d_actions);
-      hipLaunchKernelGGL((k_env_fixup<MASK_STORED>), g, dim3(64), 0, st, sd, steps, d_rng, d_actions);
+      hipLaunchKernelGGL((k_env_fixup<MASK_STORED>), gf, dim3(64), 0, st, sd, steps, d_rng, d_actions, epw);
     } else if (kind == RK_TRIO) {                          // selected masks, >= 3 players
-      const int epw = trio_epw(s.n);
-      const dim3 gt(blocks_for(s.n, epw));
       // (k_env_fixup inside the trio launch, for shards of one workgroup per CU -- inlined, or as a
       // never-inlined call -- was slower: 20-step launch at 8,192 44.2 / 42.0 against 41.3 us,
       // profiles/r04t_trio_fused.txt)
-      hipLaunchKernelGGL((k_env_rollout_trio<MASK_SELECTED>), gt, dim3(256), 0, st, sd, steps, epw, d_rng, d_actions);
-      hipLaunchKernelGGL((k_env_fixup<MASK_SELECTED>), g, dim3(64), 0, st, sd, steps, d_rng, d_actions);
+      hipLaunchKernelGGL((k_env_rollout_trio<MASK_SELECTED>), g, dim3(256), 0, st, sd, steps, epw, d_rng, d_actions);
+      hipLaunchKernelGGL((k_env_fixup<MASK_SELECTED>), gf, dim3(64), 0, st, sd, steps, d_rng, d_actions, epw);
     } else {
       hipLaunchKernelGGL((k_env_rollout_duo<MASK_SELECTED>), g, dim3(128), 0, st, sd, steps, d_rng, d_actions);
-      hipLaunchKernelGGL((k_env_fixup<MASK_SELECTED>), g, dim3(64), 0, st, sd, steps, d_rng, d_actions);
+      hipLaunchKernelGGL((k_env_fixup<MASK_SELECTED>), gf, dim3(64), 0, st, sd, steps, d_rng, d_actions, epw);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }

@@ -117,9 +117,19 @@ static std::vector<int> devices_of(const py::object &device, size_t) {
   return out;
 }
 
+// The env's outputs are read-only views (writeable=False): the reference's views alias the live
+// engine state (common.h:98-101), so a write there changes the game; here the records live in HBM
+// and the pinned views are the engine's copies, which it never reads back -- a write would be
+// silently lost, so numpy refuses it instead ("assignment destination is read-only").  Inputs the
+// caller fills (the sampler's actions, passed to env.step) stay writable.
+static py::array readonly(py::array a) {
+  a.attr("setflags")("write"_a = false);
+  return a;
+}
 template <class T>
-static py::array view(T *ptr, size_t n, py::handle base) {
-  return py::array_t<T>({(py::ssize_t)n}, {(py::ssize_t)sizeof(T)}, ptr, base);
+static py::array view(T *ptr, size_t n, py::handle base, bool writeable = false) {
+  py::array a = py::array_t<T>({(py::ssize_t)n}, {(py::ssize_t)sizeof(T)}, ptr, base);
+  return writeable ? a : readonly(a);
 }
 
 template <class T>
@@ -389,7 +399,8 @@ PYBIND11_MODULE(_city_of_gold, m) {
       .def_property_readonly("rewards", [](py::object self) {
         VecEnv &e = self.cast<VecEnv &>();
         auto v = e.views();
-        return py::array_t<float>({(py::ssize_t)v.n_envs, (py::ssize_t)4}, {(py::ssize_t)16, (py::ssize_t)4}, v.rewards, self);
+        return readonly(py::array_t<float>({(py::ssize_t)v.n_envs, (py::ssize_t)4}, {(py::ssize_t)16, (py::ssize_t)4},
+                                           v.rewards, self));
       })
       .def_property_readonly("infos", [](py::object self) {
         VecEnv &e = self.cast<VecEnv &>();
@@ -461,7 +472,7 @@ PYBIND11_MODULE(_city_of_gold, m) {
            "device"_a = py::none())
       .def("get_actions", [](py::object self) {
         VecSampler &s = self.cast<VecSampler &>();
-        return view(s.actions(), s.num_envs(), self);
+        return view(s.actions(), s.num_envs(), self, true);   // an input of env.step: writable
       })
       .def("sample", &VecSampler::sample, "action_mask"_a)
       .def("device_actions", [](VecSampler &s, int k) {

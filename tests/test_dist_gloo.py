@@ -95,9 +95,11 @@ def test_shard_blocks():
 
 
 def test_bench_roofline_store_model():
-    """bench.roofline: HBM by SURVEY 8d's 800 B/env-step; the counter traffic and round 3's store
-    model from the profile entry of the launch's own shape (envs, steps per launch, rollout kind);
-    nulls (with a note) for a shape or kernel the profile did not measure."""
+    """bench.roofline: HBM by the counter-measured bytes of the launch's own shape (envs, steps per
+    launch, rollout kind) over the launch time, frac <= 1 for any real traffic; SURVEY 8d's 800
+    B/env-step as a labelled equivalent; round 3's store model; the limiter's busy fraction from a
+    stamps profile of the shape; nulls (with a note) for a shape or kernel the profile did not
+    measure."""
     import bench
     n, k, launch = 65536, 20, 100e-6
     prof = {"store_costs": {"c_hit_s": 5e-12, "c_miss_s": 16e-12},
@@ -107,21 +109,25 @@ def test_bench_roofline_store_model():
                          "8192:20": {"kind": "duo", "envs": 8192, "chunk": k, "bytes_per_launch": 2.0e7,
                                      "companion": {"bytes_per_launch": 1.0e6},
                                      "l2_per_launch": {"writes": 1.0e6, "hits": 1.0e6, "misses": 1.0e4}}}}
-    r = bench.roofline(prof, n, k, launch, "trio")
+    stamps = {"shapes": {"65536": {"busy_ticks_per_step": 3000.0, "wait_ticks_per_step": 600.0,
+                                   "ticks_per_step": 3600.0, "busy_frac": 3000.0 / 3600.0}}}
+    r = bench.roofline(prof, n, k, launch, "trio", stamps)
     alg = 800 * n * k
-    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
-    assert abs(r["achieved"] - alg / launch / 1e9) < 1e-9 * r["achieved"]
-    assert abs(r["frac"] - r["achieved"] / 8000.0) < 1e-12 and r["traffic"] == 3.6e8
-    assert abs(r["counter_frac"] - 3.6e8 / launch / 1e9 / 8000.0) < 1e-12
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0 and r["traffic"] == 3.6e8
+    assert abs(r["achieved"] - 3.6e8 / launch / 1e9) < 1e-9 * r["achieved"]
+    assert abs(r["frac"] - r["achieved"] / 8000.0) < 1e-12 and 0 < r["frac"] <= 1
+    assert abs(r["survey_8d_equivalent"]["GBs"] - alg / launch / 1e9) < 1e-6
+    assert r["limiter"]["busy_frac"] == 3000.0 / 3600.0
     t_store = 4.5e6 * 5e-12 + 3.5e6 * 16e-12
     assert abs(r["store_model"]["frac"] - t_store / launch) < 1e-12
     assert abs(r["env_steps_per_s"] - n * k / launch) < 1e-6 * r["env_steps_per_s"]
     assert r["valu_issue"]["valu_per_wave_step"] == 1000.0 and r["kernel"].startswith("k_env_rollout_trio")
     small = bench.roofline(prof, 8192, k, 50e-6, "duo")            # its own entry, not the 65,536 one
     assert small["traffic"] == 2.1e7 and small["kernel"].startswith("k_env_rollout_duo")
+    assert "busy_frac" not in small["limiter"]
     assert abs(small["store_model"]["frac"] - (1.0e6 * 5e-12 + 1.0e4 * 16e-12) / 50e-6) < 1e-12
     for other in (bench.roofline(prof, 16384, k, launch, "duo"),       # shape not profiled
                   bench.roofline(prof, 8192, k, launch, "pipe"),       # profiled with another kernel
                   bench.roofline(prof, n, 1000, launch, "trio")):      # another launch length
         assert other["traffic"] is None and other["store_model"] is None and "traffic unknown" in other["note"]
-        assert other["frac"] > 0
+        assert other["frac"] is None and other["survey_8d_equivalent"]["x_peak"] > 0

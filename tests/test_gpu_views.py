@@ -1,0 +1,100 @@
+"""GPU: the host views are honest about writes.
+
+The reference's views alias the live engine state (include/pybind/common.h:98-101): a write into
+`selected_action_masks` changes the deck's mask that `step` reads (src/player.cpp:16-27).  Here
+the env's records live in HBM and the numpy views are pinned copies the engine never reads back,
+so the env's output views are read-only: an in-place write raises instead of being silently
+lost.  Inputs stay writable and are honoured: the sampler's actions view (the argument of
+env.step), and masks a caller edits in a copy before `sampler.sample(masks)` -- both checked
+against the C oracle fed the same edited bytes.  Also: the sampler handed the env's own mask view
+while an asynchronous runner.step() is still in flight reads the masks after that step (the
+sampler's stream waits for the env's), as the same calls with a sync in between do.
+"""
+import numpy as np
+import pytest
+
+import pyoracle as po
+
+pytestmark = pytest.mark.gpu
+
+
+def make(cg, n, seed, max_steps=100000):
+    env = cg.vec.get_vec_env(n)()
+    smp = cg.vec.get_vec_sampler(n)(seed)
+    env.reset(seed, 4, 3, cg.HARD, max_steps, False)
+    orc, osm = po.OracleVec(n), po.OracleSampler(n, seed)
+    orc.reset(seed, 4, 3, 2, max_steps)
+    return env, smp, orc, osm
+
+
+def test_env_output_views_are_read_only(cg):
+    n = 64
+    env, smp, _, _ = make(cg, n, 5)
+    runner = cg.vec.get_runner(n)(env, smp, None)
+    views = {"observations": env.observations, "selected_action_masks": env.selected_action_masks,
+             "infos": env.infos, "rewards": env.rewards, "dones": env.dones,
+             "agent_selection": env.agent_selection, "runner.get_action_masks": runner.get_action_masks(),
+             "runner.get_actions": runner.get_actions()}
+    for nm, v in views.items():
+        assert not v.flags.writeable, nm
+    with pytest.raises(ValueError):
+        env.selected_action_masks["play"][:, 1] = False
+    with pytest.raises(ValueError):
+        env.observations["shared"]["phase"][0] = 2
+    with pytest.raises(ValueError):
+        env.rewards[0, 0] = 1.0
+    with pytest.raises(ValueError):
+        cg.ActionMask(env.selected_action_masks[3, ...]).play = np.zeros(22, bool)   # record views too
+    assert smp.get_actions().flags.writeable                 # an input of env.step
+
+
+def test_edited_inputs_are_honoured(cg):
+    """Masks edited in a copy and actions edited in the sampler's view reach the engine exactly as
+    the oracle takes the same bytes."""
+    n, seed = 128, 77
+    env, smp, orc, osm = make(cg, n, seed)
+    acts = smp.get_actions()
+    rng = np.random.default_rng(1)
+    for t in range(60):
+        masks = env.selected_action_masks.copy()             # a caller's own masks, edited
+        omasks = orc.selected_action_masks.copy()
+        drop = rng.random(n) < 0.5
+        masks["play"][drop, 0] = False                       # forbid passing for half the envs (where
+        omasks["play"][drop, 0] = False                      # a card is playable the sample still succeeds)
+        keep = masks["play"].any(axis=1)
+        masks["play"][~keep, 0] = True
+        omasks["play"][~keep, 0] = True
+        smp.sample(masks)
+        osm.sample(omasks)
+        assert po.named_equal(acts, osm.actions) is None, f"sample of edited masks differs at step {t}"
+        if t % 3 == 0:                                       # an edited action: pass instead
+            acts["play"][::7] = 0
+            osm.actions["play"][::7] = 0
+        env.step(acts)
+        orc.step(osm.actions)
+        for nm in ("observations", "selected_action_masks", "infos"):
+            bad = po.named_equal(getattr(env, nm), getattr(orc, nm))
+            assert bad is None, f"step {t}: {nm}.{bad} differs from the oracle"
+        assert np.array_equal(env.agent_selection, orc.agent_selection)
+
+
+def test_sampler_on_env_view_orders_after_async_step(cg):
+    """runner.sample(); runner.step() (asynchronous, publishes itself); then sampler.sample on the
+    env's own mask view without a sync: the sampler reads the masks after that step."""
+    n, seed = 256, 31
+    env, smp, orc, osm = make(cg, n, seed)
+    smp2 = cg.vec.get_vec_sampler(n)(1000)
+    osm2 = po.OracleSampler(n, 1000)
+    runner = cg.vec.get_runner(n)(env, smp, None)
+    masks = env.selected_action_masks
+    for t in range(40):
+        runner.sample()
+        runner.step()                                        # in flight
+        smp2.sample(masks)                                   # the env's own view: HBM, ordered
+        osm.sample(orc.selected_action_masks)
+        orc.step(osm.actions)
+        osm2.sample(orc.selected_action_masks)
+        runner.sync()
+        assert po.named_equal(smp2.get_actions(), osm2.actions) is None, f"step {t}: sampled before the step"
+        bad = po.named_equal(env.selected_action_masks, orc.selected_action_masks)
+        assert bad is None, f"step {t}: {bad}"
