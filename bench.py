@@ -28,10 +28,14 @@ Also reported (rank 0; the extra lines only at N=1, so a scaling run stays short
   host_loop      the reference's numpy loop through the host API at C2 (256, EASY) and the C4
                  shard (8,192, HARD, runner.sample(); runner.step_sync()), D2H bytes per step
   full_dynamics  stored-mask driver (moves, shop, specials), max_steps 30: auto-resets with
-                 device map generation inside the rollout
+                 device map generation inside the rollout; full_dynamics_steady the same driver
+                 with max_steps 100,000 (no constant resets), 1,000-step launches
   reset, sample  time_reset / time_sample equivalents (benchmarks/benchmarks.py:53-69); reset()
                  without arguments beside reset(seed, ...); time_reset_C2 the asv shape (256 EASY)
   peakmem        asv peakmem_runner: device and host bytes of a runner with host views
+  asv_grid       asv time_run / time_sample (benchmarks.py:47-57) at N in {1, 8, 64, 256, 8192} x
+                 {sequential, async, sync}, 10,000 steps each, EASY; the N where each mode passes
+                 cpu_baseline
   encode         the map-observation encode kernel (reset path), 18,432 B/env, beside a measured
                  device copy peak
   cpu_baseline   the C oracle (port of the reference) on the host cores in the reference
@@ -70,6 +74,7 @@ def parse():
     ap.add_argument("--chunk", type=int, default=1000, help="rollout steps per kernel launch")
     ap.add_argument("--no-extras", action="store_true", help="headline + roofline only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-asv", action="store_true", help="skip the asv time_run / time_sample grid extra")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline wall time")
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="only run warmup + this many rollout steps (rocprofv3 captures); no JSON checks")
@@ -245,6 +250,69 @@ def time_reset_c2(cg, dev, calls=100):
     del env
     return {"envs": n, "calls": calls, "ms_per_call": s * 1e3, "resets_per_s": n / s,
             "note": "vec_cog_env_256.reset() x calls (asv TimeEnvs.time_reset, sequential)"}
+
+
+ASV_NS = (1, 8, 64, 256, 8192)
+ASV_MODES = ("sequential", "async", "sync")
+ASV_STEPS = 10000                  # benchmarks.py:5 N_STEPS
+
+
+def asv_setup(cg, n, mode, dev):
+    """TimeEnvs.setup (benchmarks/benchmarks.py:16-45) for (n, seed 12345, mode): the sample / step /
+    end / sync callables of one mode, EASY maps, 4 players, 3 pieces.  The GPU runner has no thread
+    count (its work runs on the device's stream), so `threads` is 1 throughout."""
+    env = cg.vec.get_vec_env(n)(device=dev)
+    env.reset(SEED, N_PLAYERS, N_PIECES, cg.EASY, MAX_STEPS, False)
+    smp = cg.vec.get_vec_sampler(n)(SEED, device=dev)
+    acts, am = smp.get_actions(), env.selected_action_masks
+    if mode == "sequential":
+        return (env, smp), (lambda: smp.sample(am)), (lambda: env.step(acts)), (lambda: None), (lambda: None)
+    runner = cg.vec.get_runner(n)(env, smp, 1)
+    if mode == "sync":
+        return (env, smp, runner), runner.sample, runner.step_sync, (lambda: None), runner.sync
+    return (env, smp, runner), runner.sample, runner.step, runner.sync, (lambda: None)
+
+
+def asv_grid(cg, dev, cpu_value=None, steps=ASV_STEPS):
+    """asv TimeEnvs.time_run and time_sample (benchmarks/benchmarks.py:47-57) over N in ASV_NS and
+    the three modes, exactly as the reference defines them: sequential = sampler.sample(masks);
+    env.step(actions) per step; async = runner.sample(); runner.step() per step, one runner.sync()
+    at the end; sync = runner.sample(); runner.step_sync() per step.  time_sample: the sample call
+    (+ sync() in sync mode) per step.  env-steps/s = N x steps / wall.  `crossover`: per mode, the
+    smallest N of the grid whose time_run rate passes the CPU baseline (cpu_value, env-steps/s)."""
+    out = {"steps": steps, "threads": 1, "Ns": list(ASV_NS), "time_run": {}, "time_sample": {}}
+    for mode in ASV_MODES:
+        out["time_run"][mode], out["time_sample"][mode] = {}, {}
+        for n in ASV_NS:
+            keep, sample, step, end, sync = asv_setup(cg, n, mode, dev)
+            for _ in range(20):                              # warm-up (not in asv: its own repeats)
+                sample()
+                step()
+            end()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                sample()
+                step()
+            end()
+            run = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                sample()
+                sync()
+            end()
+            smp_s = time.perf_counter() - t0
+            out["time_run"][mode][str(n)] = {"s": run, "us_per_step": run / steps * 1e6,
+                                             "env_steps_per_s": n * steps / run}
+            out["time_sample"][mode][str(n)] = {"s": smp_s, "us_per_call": smp_s / steps * 1e6,
+                                                "samples_per_s": n * steps / smp_s}
+            del keep, sample, step, end, sync
+    if cpu_value:
+        out["cpu_baseline_env_steps_per_s"] = cpu_value
+        out["crossover"] = {m: next((n for n in ASV_NS if out["time_run"][m][str(n)]["env_steps_per_s"] > cpu_value),
+                                    None) for m in ASV_MODES}
+        out["crossover_note"] = ("smallest N of the grid whose time_run rate passes cpu_baseline (the C port in the "
+                                 "reference ThreadedRunner shape, best thread count); null: none of the grid")
+    return out
 
 
 def rss_bytes():
@@ -559,6 +627,25 @@ def main():
                                    "workload": f"{n} envs, 4p HARD, max_steps 30, stored-mask sampler, "
                                                "500-step launches, auto-reset with device map generation",
                                    "envs_with_a_finished_episode": resets}
+        del runner, smp, env
+        # full dynamics without the constant resets: stored masks, max_steps 100,000 (episodes of the
+        # reference harness's length), 1,000-step launches -- the general step's own rate
+        env, smp, runner = make(cg, n, base, dev, stored=True)
+        runner.set_chunk(1000)
+        runner.rollout(200)
+        d.barrier_sync(runner)
+        fs_steps = 2000
+        t1 = time.perf_counter()
+        runner.rollout(fs_steps)
+        d.barrier_sync(runner)
+        fs_wall = time.perf_counter() - t1
+        fs_kern = kernel_time(runner, 1000, 2)
+        extras["full_dynamics_steady"] = {
+            "value": n * fs_steps / fs_wall, "unit": "env-steps/s", "ms_per_step": fs_wall / fs_steps * 1e3,
+            "steps": fs_steps, "kernel_us_per_step": fs_kern / 1000 * 1e6,
+            "rollout_kind": cg._city_of_gold.rollout_kind(n, N_PLAYERS, True),
+            "workload": f"{n} envs, 4p HARD, max_steps 100000, stored-mask sampler (moves, purchases, specials: "
+                        "test_environment.cpp:95-101's driver), 1,000-step launches"}
         # time_reset / time_sample (benchmarks/benchmarks.py:53-69)
         t1 = time.perf_counter()
         reps = 5
@@ -590,11 +677,21 @@ def main():
             "C4_shard": host_loop(cg, N_SHARD8, cg.HARD, dev, 100, True)}
         extras["time_reset_C2"] = time_reset_c2(cg, dev)
         extras["peakmem"] = peakmem(cg, d, n, dev)
+        if not args.no_asv:
+            extras["asv_grid"] = asv_grid(cg, dev)
 
     if d.rank == 0:
         cpu = None
         if d.world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.cpu_seconds)
+            g = extras.get("asv_grid")
+            if g:                                          # the crossover N against the same baseline
+                ref = cpu["value"]
+                g["cpu_baseline_env_steps_per_s"] = ref
+                g["crossover"] = {m: next((n for n in ASV_NS if g["time_run"][m][str(n)]["env_steps_per_s"] > ref),
+                                          None) for m in ASV_MODES}
+                g["crossover_note"] = ("smallest N of the grid whose time_run rate passes cpu_baseline (the C port "
+                                       "in the reference ThreadedRunner shape, best thread count); null: none")
         out = {
             "metric": METRIC,
             "value": value,

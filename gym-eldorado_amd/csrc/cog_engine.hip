@@ -1443,9 +1443,8 @@ DEV void sample_heads(const Heads &h, uint32_t &rng, uint8_t out[5], const UidEn
 // draws, so the sampler's state two steps on is known before those steps run: the storing wave
 // computes, from the state a step record carries, the five draws of the step after next
 // (presample: the state they start from, head 0's draw, the state after the five, and whether any
-// draw could be rejected) and the stepping wave samples from them (sample_presampled) when its
-// state is the one they start from and every head is non-empty -- else, or when a head other than
-// head 0 holds two or more candidates, it draws the sequential way (sample_heads).  The values
+// draw could be rejected) and the stepping wave samples from them (sample_lean) when its state is
+// the one they start from and heads 1-4 are {0} -- else it draws the sequential way (sample_heads).  The values
 // are the same either way (cog_rng.h jump-ahead: x * 16807^j mod (2^31 - 1)).
 constexpr uint32_t kPow15 = mr_pow(15);
 DEV uint4 presample(uint32_t x) {                          // x: the state the step starts from
@@ -1457,22 +1456,6 @@ DEV uint4 presample(uint32_t x) {                          // x: the state the s
     risk |= r >= kSmallSafe ? 1u : 0u;
   }
   return make_uint4(x, r0, y, risk);
-}
-// act[0..4] from the presampled draws; false: not applicable (the caller samples sequentially)
-DEV bool sample_presampled(const Heads &h, const uint4 &pre, uint32_t &rng, uint8_t out[5], const UidEntry *tab) {
-  const uint32_t m[5] = {h.play, h.spec, h.rem, h.move, h.shop};
-  bool ok = pre.x == rng && pre.w == 0u;
-#pragma unroll
-  for (int j = 1; j < 5; j++) ok = ok && __popc(m[j]) == 1;  // heads 1-4: one candidate each
-  const uint32_t k0 = __popc(m[0]);
-  ok = ok && k0 >= 1u;
-  if (!ok) return false;
-  const UidEntry e0 = tab[k0];
-  out[0] = (uint8_t)(k0 >= 2u ? nth_set_bit(m[0], uid_tab_accepted(pre.y, e0.s, e0.m)) : (uint32_t)(__ffs(m[0]) - 1));
-#pragma unroll
-  for (int j = 1; j < 5; j++) out[j] = (uint8_t)(__ffs(m[j]) - 1);
-  rng = pre.z;
-  return true;
 }
 DEV void sample_mask(const uint8_t *mask, uint32_t &rng, uint8_t out[5], const UidEntry *tab) {
   sample_heads(heads_of(mbits_from_bytes(mask)), rng, out, tab);
@@ -2257,62 +2240,17 @@ DEV bool step_regs(RegEnv &R, const uint8_t act[5], const DevState &s, size_t i,
   return COG_HEX_END(c0) || R.turn_counter >= R.max_steps;
 }
 
-// The trio's step (k_env_rollout_trio): cog_env::step (environment.cpp:91-224) for an action that
-// plays a card or passes, by a player with no move, free card, free move or pending removes in
-// progress and who has not won (lean_ok) -- every step of the canonical selected-mask loop
-// (SURVEY Q1); any other env is parked before its step (kParkRedo) and run by the full step.
-// Three parts of the reference's step are left to the other waves: the deck's piles other than the
-// hand (the drawing wave replays the play on its copy of the deck, trio_drawer), the turn end's
-// discard + draws (the drawing wave too) and update_observation's movement / shop heads of the acting
-// player's stored mask when the turn goes on -- with the selected masks nothing reads those
-// heads but the output record (save_actionmask replaces them at the turn end), so the storing
+// The trio's step (k_env_rollout_trio, trio_stepper's loop): cog_env::step (environment.cpp:91-224)
+// for an action that plays a card or passes, by a player with no move, free card, free move or
+// pending removes in progress and who has not won (lean_player) -- every step of the canonical
+// selected-mask loop; any other env is parked before its step (kParkRedo) and run by
+// the full step.  Three parts of the reference's step are left to the other waves: the deck's piles
+// other than the hand (the drawing wave replays the play on its copy of the deck, trio_drawer), the
+// turn end's discard + draws (the drawing wave too) and update_observation's movement / shop heads
+// of the acting player's stored mask when the turn goes on -- with the selected masks nothing reads
+// those heads but the output record (save_actionmask replaces them at the turn end), so the storing
 // wave computes them from the step record (trio_storer).  At a turn end the new agent's stored
-// mask gets update_observation's values for the INACTIVE phase (move = shop = {0}) here.
-DEV bool lean_ok(const RegEnv &R, const uint8_t act[5]) {
-  return ((uint32_t)act[1] | act[2] | act[3] | act[4] | R.P.next_move_free | R.P.next_card_free | R.P.n_removes |
-          R.P.mip | R.P.has_won) == 0u;
-}
-DEV bool step_lean(RegEnv &R, int a_play, int na, bool &turn_end) {   // (R.d: the hand pile only)
-  const int ag = (int)R.agent();
-  PState &P = R.P;
-  const uint32_t info = ((R.info_steps >> (8 * ag)) + 1u) & 0xffu;   // Info steps_taken (u8)
-  R.info_steps = (R.info_steps & ~(0xffu << (8 * ag))) | (info << (8 * ag));
-  uint32_t phase = R.sh[0] & 0xffu;
-  if (phase == COG_PHASE_INACTIVE) phase = COG_PHASE_MOVEMENT;
-  P.steps_taken = (P.steps_taken + 1) & 0xffu;
-  float r0 = __uint_as_float(R.sh[1]), r1 = __uint_as_float(R.sh[2]), r2 = __uint_as_float(R.sh[3]);
-  if (a_play > 8) P.pad = 1u;                              // the deck's "wide" flag (step_regs)
-  if (a_play) {                                            // Player::play_card (player.cpp:45-60)
-    const int c = a_play - 1;
-    if (phase == COG_PHASE_MOVEMENT) {
-      r0 = (float)cardf(kRes0, c); r1 = (float)cardf(kRes1, c); r2 = (float)cardf(kRes2, c);
-    } else if (phase == COG_PHASE_BUYING) {
-      const uint32_t coin = cardf(kRes2, c);
-      r2 = r2 + (coin > 0 ? (float)coin : 0.5f);
-    }
-    R.leave_hand(c, false);                                // Deck::activate (the active pile: the
-    P.n_active = (P.n_active + 1) & 0xffu;                 // drawing wave replays it, trio_drawer)
-    P.idx_last = (uint32_t)c;
-  } else {
-    phase = (phase + 1) % 3;                               // pass: next phase
-  }
-  turn_end = phase == COG_PHASE_INACTIVE;                  // maybe_end_turn -> next_agent
-  if (turn_end) {
-    P.n_active = 0;                                        // Player::end_turn (the deck: drawing wave)
-    R.sta = R.sel;                                         // save_actionmask
-    R.set_agent((uint32_t)na);
-    R.sel = R.stn;                                         // load_actionmask (na != ag: >= 3 players)
-    R.stn.move = 1u;                                       // update_observation, INACTIVE phase
-    R.stn.shop = 1u;
-    r0 = r1 = r2 = 0.f;
-    R.turn_counter++;
-  }
-  R.sh[0] = (R.sh[0] & ~0xffu) | phase;
-  R.sh[1] = __float_as_uint(r0); R.sh[2] = __float_as_uint(r1); R.sh[3] = __float_as_uint(r2);
-  const uint2 cc = turn_end ? R.cells_n : R.cells_a;      // (a copy: a reference picked between two
-  const uint32_t c0 = R.use_cell(cc, 0);                   // members would keep R out of registers)
-  return COG_HEX_END(c0) || R.turn_counter >= R.max_steps;
-}
+// mask gets update_observation's values for the INACTIVE phase (move = shop = {0}) in the stepper.
 
 // ---- lane drivers ---------------------------------------------------------------------------
 // Snap: the step-start image of everything a step may modify; the store phase writes back the
@@ -2799,7 +2737,7 @@ DEV void lds_players(const LaneLds &L, int l, int ag, int na, Snap &S) {
 // the fix-up as a second kernel: 4.8 us per launch even when it had nothing to do).
 // park codes: bits 0..29 the step t; kParkFinish: step t finished the episode (else the env
 // started step t done); kParkRedo: step t was not run (the trio's stepping wave met an action
-// outside its lean step, lean_ok in trio_stepper) -- the fix-up runs it with the full step
+// outside its lean step, lean_player in trio_stepper) -- the fix-up runs it with the full step
 constexpr uint32_t kParkNone = ~0u, kParkFinish = 1u << 31, kParkRedo = 1u << 30;
 constexpr uint32_t kParkStep = kParkRedo - 1u;
 // The records of a wave's envs seen from the wave's first env: a per-wave (scalar) base and a
@@ -3237,7 +3175,7 @@ DEV void duo_store_env_private(const DevState &s, size_t i, const RegEnv &R) {
 // then the saved mask gains the drawn cards (draw's mask updates, cards.cpp:183-211, precede
 // save_actionmask).  Nothing the stepping wave reads before that player acts again depends on it:
 // with >= 3 players the next two agents are other players, whose turn ends lie at least two steps
-// back.  Any action outside the lean step (lean_ok: never in the canonical loop) parks
+// back.  Any action outside the lean step (lean_player: never in the canonical loop) parks
 // the env with kParkRedo, and k_env_fixup runs that step and the rest with the full step.
 
 template <int SRC>
@@ -3527,7 +3465,7 @@ __global__ void __launch_bounds__(128) k_env_rollout_duo(DevState s, int steps, 
 // ------------------------------------------------------------------------------------------
 // Trio rollout (round 4): the selected-mask loop with >= 3 players at every shard size (cog_rollout_kind),
 // one step's work spread over four waves per 64 envs.  The stepping wave runs the lean step
-// (step_lean: sample, play or pass, turn change, done check) and nothing else; the drawing wave
+// (the lean step: sample, play or pass, turn change, done check) and nothing else; the drawing wave
 // owns the decks (replays each play on its copy, runs the turn ends' discard + draws with the env
 // rng); two storing waves issue the store phase, one of them also producing the sampler's
 // presampled draws (presample).  History (8,192 envs, device us per step in 1,000-step launches,
@@ -3538,14 +3476,15 @@ __global__ void __launch_bounds__(128) k_env_rollout_duo(DevState s, int steps, 
 // round is as long as the two it replaces); decoupled through progress counters (below).
 //
 // The waves run as a pipeline over LDS buffers, synchronised by progress counters in LDS (cnt[],
-// release / acquire at workgroup scope; a waiting wave sleeps between polls) instead of barriers,
-// so each runs at its own average rate:
+// stored after the records they publish -- in-order LDS, cnt_store; a waiting wave sleeps between
+// polls) instead of barriers, so each runs at its own average rate:
 //   stepping wave  step t: ring slot t % 8 free (record t - 8 stored by both storing waves), step
 //                  t's presampled draws written (cnt[PRE] > t - 4); step; record t -> ring,
 //                  cnt[REC] = t + 1; at a turn change, the drawing wave past the last turn ends of
 //                  the new agent (its hand, counters) and of the player after it (its stored mask,
-//                  n_active) -- per player, the step its last turn ended (tend[]); with >= 3
-//                  players and turns of >= 2 steps those lie >= 2 steps back.
+//                  hand nibbles) -- the later of the two is 1 (3 players) or 2 (4 players) turn
+//                  ends back (te1, te2); with >= 3 players and turns of >= 2 steps those lie >= 2
+//                  steps back.
 //   drawing wave   records r, r + 1 (r even) once written: the plays replayed on the acting players'
 //                  decks (img: two byte updates each), then ONE turn-end pass -- a lean turn lasts at least two steps (pass
 //                  in MOVEMENT, pass in BUYING), so a player ends at most one turn in two records --
@@ -3566,7 +3505,7 @@ __global__ void __launch_bounds__(128) k_env_rollout_duo(DevState s, int steps, 
 // mask bits + meta, 2 the acting player's stored-mask bits (saved mask at a turn end: the drawing
 // wave adds the drawn cards) + action byte 0 + n_active of the acting player << 8 + the deck
 // granules the record changed << 16 (drawing wave).  The next player's stored mask changes only at a
-// turn end, by fixed heads (step_lean), so storing wave A derives it from its own image.  The
+// turn end, by fixed heads (the lean step), so storing wave A derives it from its own image.  The
 // neighbourhood caches never change in the lean step (no moves): the stepping wave and storing wave
 // A keep their own copies, and the epilogue does not store them.  The stepping wave's player
 // counters go to LDS only at a turn end (the drawing wave's) and at a park or the end (the epilogue's).
@@ -3589,6 +3528,8 @@ struct TrioLds {
   uint3 pre[kTrioLead][64];           // step t's presampled draws, t % 4: state, head 0's draw | risk << 31, state after
   uint4 pl[4][64];
   uint4 heads[4][64];
+  uint4 hand4[4][64];                 // every player's hand as nibbles (hand_nibbles: the drawing wave's)
+  uint4 stbA[4][64];                  // storing wave A: every player's stored mask as last stored (bits)
   uint32_t flg[64];                   // the other waves' hazard flags (the stepping wave's epilogue)
   uint32_t cnt[kTrioCnts];            // progress counters
   UidEntry tab[kUidTab];
@@ -3615,12 +3556,21 @@ DEV void cnt_read(const TrioLds &D, TrioCnt6 &c) {
   c.fin = __builtin_amdgcn_readfirstlane(v[CNT_FIN]);
   c.abort = __builtin_amdgcn_readfirstlane(v[CNT_ABORT]);
 }
-// Publishes this wave's earlier LDS writes, all lanes' included, through lane 0's release store.
-// That relies on the wave executing as one: the release's s_waitcnt lgkmcnt(0) is issued by the
-// wave and covers every lane's outstanding LDS writes (LDS ops of a wave complete in order), which
-// the AMDGPU backend guarantees for a wave's own ops, though the HIP memory model speaks of threads.
+// Publishes this wave's earlier LDS writes, all lanes' included, through lane 0's store of the
+// counter.  The LDS executes one wave's DS instructions in issue order (their lgkmcnt returns are
+// in order), so a wave that reads the counter's new value and then the records reads what was
+// written before it: the ordering that matters is the compiler's, which a wavefront-scope fence
+// keeps (no instruction).  A workgroup-scope release would add an s_waitcnt lgkmcnt(0) on the
+// stepping wave's path every step, waiting also for its own reads in flight ($COG_TRIO_FENCE
+// builds, -DCOG_TRIO_FENCE, keep that form for A/B).
 DEV void cnt_store(TrioLds &D, int k, uint32_t v) {
+#ifdef COG_TRIO_FENCE
   if ((threadIdx.x & 63) == 0) __hip_atomic_store(&D.cnt[k], v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_store(&D.cnt[k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
 }
 // wait (wave-uniform) until counter `field` of c (a member of c) >= v
 DEV void cnt_wait(TrioLds &D, TrioCnt6 &c, const uint32_t &field, uint32_t v, const DevState &s) {
@@ -3654,6 +3604,94 @@ DEV void trio_store_players(const TrioLds &D, const DevState &s, int ne) {
   }
 }
 
+// ---- the stepping wave's lean image (round 5) ----------------------------------------------
+// The acting player's hand as 4-bit counts (nibble c = hand[c], types 0-7 / 8-15 / 16-20 in three
+// dwords), made by the drawing wave from its deck image (hand_nibbles: at the prologue and after
+// each turn end's draws) with a flag when a count exceeds 15; the player record packed, with the
+// three counters the lean step changes unpacked; the masks as bit vectors (MBits).  A play reads
+// and decrements one nibble instead of selecting over the six dwords of the byte pile.
+struct LeanHand {
+  uint32_t w[3];
+};
+// the drawing wave: hand[0..20] of a DeckObs image (bytes 21..41) as nibbles; .w = 1 when a count
+// does not fit a nibble (the stepping wave then parks the player's steps: kParkRedo)
+DEV uint4 hand_nibbles(const uint4 g1, const uint4 g2) {
+  const uint32_t d[8] = {g1.x, g1.y, g1.z, g1.w, g2.x, g2.y, g2.z, g2.w};   // deck bytes 16..47
+  uint32_t h[6], ovf = 0u;
+#pragma unroll
+  for (int q = 0; q < 6; q++) {                            // hand bytes 4q..4q+3 (byte 21 + 4q = deck
+    uint32_t x = fsh8(d[q + 2], d[q + 1], 1);              // dword 5 + q, byte 1)
+    if (q == 5) x &= 0xffu;                                // hand[20] only (then the active pile)
+    ovf |= x & 0xf0f0f0f0u;
+    h[q] = x;
+  }
+  uint32_t w[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {                            // 8 counts per dword
+    const uint32_t lo = h[2 * k], hi = 2 * k + 1 < 6 ? h[2 * k + 1] : 0u;
+    const uint32_t a = (lo | (lo >> 4)) & 0x00ff00ffu, b = (hi | (hi >> 4)) & 0x00ff00ffu;
+    w[k] = ((a | (a >> 8)) & 0xffffu) | ((b | (b >> 8)) & 0xffffu) << 16;
+  }
+  return make_uint4(w[0], w[1], w[2], ovf ? 1u : 0u);
+}
+// card c leaves the hand (Deck::activate's hand part, player.cpp:45-60, cards.cpp:242-253): the
+// count before (a count of 0 stays 0 here -- the reference wraps it to 255 (u8), the drawing wave's
+// byte image too, but the play bit of c is then clear and no lean step plays c again before the
+// drawing wave's next hand_nibbles, which flags the 255)
+DEV uint32_t nib_take(LeanHand &H, int c) {
+  const int q = c >> 3, sh = 4 * (c & 7);
+  const uint32_t w = q == 0 ? H.w[0] : (q == 1 ? H.w[1] : H.w[2]);
+  const uint32_t prev = (w >> sh) & 0xfu;
+  const uint32_t nw = w - ((prev ? 1u : 0u) << sh);
+  H.w[0] = q == 0 ? nw : H.w[0];
+  H.w[1] = q == 1 ? nw : H.w[1];
+  H.w[2] = q == 2 ? nw : H.w[2];
+  return prev;
+}
+// the selected mask's heads 1-4 are {0} (special, remove, move, shop: MBits bits 22.., w1, w2)
+DEV bool heads14_zero(const MBits &b) { return (b.w0 >> 22) == 1u && b.w1 == (1u << 12) && b.w2 == 0x204u; }
+constexpr uint32_t kMoveShopBits = (0x7fu << 2) | (0x7ffffu << 9);   // MBits w2: move and shop heads
+// the j-th set bit of m (j < popc(m)): clear the lowest set bit j times, as many rounds as the
+// wave's largest j (the play head holds the pass bit and the hand's types: j <= 3 in the canonical
+// loop, where the binary search of nth_set_bit costs five full rounds)
+DEV uint32_t nth_set_bit_iter(uint32_t m, uint32_t j) {
+  while (__builtin_amdgcn_ballot_w64(j != 0u)) {
+    m = j ? (m & (m - 1u)) : m;
+    j = j ? j - 1u : 0u;
+  }
+  return (uint32_t)(__ffs(m) - 1);
+}
+// head 0's draw from the presampled record when the state is the one it starts from and heads
+// 1-4 are {0} (then the five draws are the presampled ones: act 1-4 = 0); false: sample the
+// sequential way
+DEV bool sample_lean(const MBits &sel, const uint3 &pr, uint32_t &rng, uint32_t &a0, const UidEntry *tab) {
+  const uint32_t m0 = sel.w0 & 0x3fffffu, k0 = __popc(m0);
+  if (!(pr.x == rng && (pr.y >> 31) == 0u && heads14_zero(sel) && k0 >= 1u)) return false;
+  const UidEntry e0 = tab[k0];
+  const uint32_t j = k0 >= 2u ? uid_tab_accepted(pr.y & 0x7fffffffu, e0.s, e0.m) : 0u;
+  a0 = nth_set_bit_iter(m0, j);
+  rng = pr.z;
+  return true;
+}
+DEV uint4 pack_lean_player(uint4 pp, uint32_t n_in_hand, uint32_t n_active, uint32_t steps_taken) {
+  pp.y = (pp.y & 0xff0000ffu) | (n_in_hand & 0xffu) << 8 | (n_active & 0xffu) << 16;
+  pp.z = (pp.z & 0xffff00ffu) | (steps_taken & 0xffu) << 8;
+  return pp;
+}
+// the lean step may run for this player: no move, free card, free move or pending removes in
+// progress, has not won (PlayerPriv x: has_won, mip, n_removes, next_card_free; y byte 0:
+// next_move_free), and its hand counts fit the nibbles
+DEV bool lean_player(const uint4 &pp, uint32_t hand_ovf) { return (pp.x | (pp.y & 0xffu) | hand_ovf) == 0u; }
+// the env-level private records from the stepping wave (duo_store_env_private<true> with the
+// selected mask as bits)
+DEV void trio_store_private(const DevState &s, size_t i, const RegEnv &R, const MBits &selb) {
+  uint4 *pw = reinterpret_cast<uint4 *>(s.priv + i);
+  reinterpret_cast<uint3 *>(reinterpret_cast<uint32_t *>(pw) + 1)[0] = make_uint3(R.seed, R.max_steps, R.turn_counter);
+  pw[1] = make_uint4(R.g1x, R.g1y, R.in_market, R.flags);
+  reinterpret_cast<uint32_t *>(pw + 3)[0] = R.info_steps;
+  s.heads[5 * i] = mbits_u4(selb);
+}
+
 template <int SRC>
 DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, uint32_t *__restrict__ rngs_glob) {
   const int l = (int)(threadIdx.x & 63);
@@ -3664,10 +3702,19 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
   uint32_t *__restrict__ rngs = rngs_glob + wbase;
   bool live = l < ne;
   uint32_t park = kParkNone, srng = 0;
-  RegEnv R;
+  PH_DECL;                                                 // (diagnostic builds: phase stamps)
+  RegEnv R;                                                // env level (the lean image below)
   uint2 cells[4];                                          // every player's neighbourhood cache
-  int tend[4] = {-1, -1, -1, -1};                          // per player: the step its last turn ended
+  // the steps of the last two turn ends before the current step (-1: none in this launch); the
+  // lean loop passes the turn strictly in order, so the last turn end of the player after the next
+  // agent -- the later of the two records the turn change reads -- lies 1 (3 players) or 2 (4
+  // players) turn ends back
+  int te1 = -1, te2 = -1;
   int ag = 0, na = 0;
+  MBits selb = {0u, 0u, 0u}, stab = selb, stnb = selb;     // selected, stored(ag), stored(na)
+  uint4 pp = make_uint4(0u, 0u, 0u, 0u);                   // PlayerPriv of ag (packed)
+  uint32_t n_in_hand = 0u, n_active = 0u, steps_taken = 0u;
+  uint2 cells_a = make_uint2(0u, 0u), cells_n = cells_a;   // ag's and na's neighbourhoods (the done check)
   if (live) {
     Snap S;
     load_env(s, i, S);
@@ -3682,32 +3729,33 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     srng = rngs[i];
     ag = (int)R.agent();
     na = (int)next_player((uint32_t)ag, R.n_players());
-    R.P = unpack_player(D.pl[ag][l]);
-    R.na_active = (D.pl[na][l].y >> 16) & 0xffu;
+    pp = D.pl[ag][l];
+    n_in_hand = (pp.y >> 8) & 0xffu;
+    n_active = (pp.y >> 16) & 0xffu;
+    steps_taken = (pp.z >> 8) & 0xffu;
     uint2 ca = cells[3], cn = cells[3];                    // (selects: no indexed registers)
 #pragma unroll
     for (int p = 2; p >= 0; p--) {
       ca = ag == p ? cells[p] : ca;
       cn = na == p ? cells[p] : cn;
     }
-    R.cells_a = ca;
-    R.cells_n = cn;
-    R.sta = heads_of(mbits_of(D.heads[ag][l]));
-    R.stn = heads_of(mbits_of(D.heads[na][l]));
+    cells_a = ca;
+    cells_n = cn;
+    selb = S.sel;
+    stab = mbits_of(D.heads[ag][l]);
+    stnb = mbits_of(D.heads[na][l]);
   }
   R.tab = D.tab;
   __builtin_amdgcn_s_waitcnt(0);                           // (no per-iteration vmcnt wait covers them)
   __syncthreads();                                         // B: every wave's prologue is done
-#pragma unroll
-  for (int k = 0; k < 28; k++) R.d[k] = 0u;                // (only the hand pile is the stepping wave's:
-  if (live) {                                              // bytes 21..41, granules 1 and 2)
-#pragma unroll
-    for (int k = 1; k < 3; k++) {
-      const uint4 v = D.img[ag][k][l];
-      R.d[4 * k] = v.x; R.d[4 * k + 1] = v.y; R.d[4 * k + 2] = v.z; R.d[4 * k + 3] = v.w;
-    }
+  LeanHand H = {{0u, 0u, 0u}};
+  bool lean_p = false;
+  if (live) {                                              // ag's hand: the drawing wave's nibbles
+    const uint4 h4 = D.hand4[ag][l];
+    H.w[0] = h4.x; H.w[1] = h4.y; H.w[2] = h4.z;
+    lean_p = lean_player(pp, h4.w);
   }
-  PH_DECL;
+  PH(6);                                                   // the prologue (to the barrier)
   TrioCnt6 cc;
   for (int t = 0; t < steps; t++) {
     const int sl = t & (kTrioDepth - 1);
@@ -3718,31 +3766,80 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     if (t >= kTrioLead) cnt_wait(D, cc, cc.pre, (uint32_t)(t - kTrioLead + 1), s_glob);
     PH(2);
     bool ended = false, finish = false, turn_end = false, stepped = false;
-    uint8_t act[5];
+    uint32_t a_play = 0u;
     if (live) {
       const uint32_t srng0 = srng;
       const uint3 pr = D.pre[t & (kTrioLead - 1)][l];
-      const bool fast =
-          sample_presampled(R.sel, make_uint4(pr.x, pr.y & 0x7fffffffu, pr.z, pr.y >> 31), srng, act, R.tab);
-      if (__builtin_amdgcn_ballot_w64(!fast) && !fast)     // (wave-uniform skip)
+      const bool fast = sample_lean(selb, pr, srng, a_play, R.tab);
+      bool other = false;                                  // an action head other than play set
+      if (__builtin_amdgcn_ballot_w64(!fast) && !fast) {   // (wave-uniform skip)
+        uint8_t act[5];
+        R.sel = heads_of(selb);
         step_action<SRC>(R, make_uint2(0u, 0u), srng, act);
+        a_play = act[0];
+        other = ((uint32_t)act[1] | act[2] | act[3] | act[4]) != 0u;
+      }
       const bool was_done = R.done() != 0u;
       // not the lean step's case (never in the canonical loop), or the test hook: hand the env to
       // k_env_fixup before its step t
-      if (!was_done && (!lean_ok(R, act) || t == s.redo_at)) {
+      if (!was_done && (!lean_p || other || t == s.redo_at)) {
         srng = srng0;
-        duo_store_env_private<true>(s, i, R);
+        trio_store_private(s, i, R, selb);
         rngs[i] = srng;
-        D.pl[ag][l] = pack_player(R.P);                    // (the epilogue's)
+        D.pl[ag][l] = pack_lean_player(pp, n_in_hand, n_active, steps_taken);   // (the epilogue's)
         park = (uint32_t)t | kParkRedo;
         live = false;
-      } else {
-        stepped = !was_done;
-        finish = stepped && step_lean(R, act[0], na, turn_end);
+      } else if (!was_done) {                              // cog_env::step, the lean case
+        stepped = true;
+        const uint32_t info = ((R.info_steps >> (8 * ag)) + 1u) & 0xffu;   // Info steps_taken (u8)
+        R.info_steps = (R.info_steps & ~(0xffu << (8 * ag))) | (info << (8 * ag));
+        uint32_t phase = R.sh[0] & 0xffu;
+        if (phase == COG_PHASE_INACTIVE) phase = COG_PHASE_MOVEMENT;
+        steps_taken = (steps_taken + 1u) & 0xffu;
+        float r0 = __uint_as_float(R.sh[1]), r1 = __uint_as_float(R.sh[2]), r2 = __uint_as_float(R.sh[3]);
+        if (a_play > 8u) pp.z = (pp.z & 0x00ffffffu) | 0x01000000u;   // the deck's "wide" flag (step_regs)
+        if (a_play) {                                      // Player::play_card (player.cpp:45-60)
+          const int c = (int)a_play - 1;
+          if (phase == COG_PHASE_MOVEMENT) {
+            r0 = (float)cardf(kRes0, c); r1 = (float)cardf(kRes1, c); r2 = (float)cardf(kRes2, c);
+          } else if (phase == COG_PHASE_BUYING) {
+            const uint32_t coin = cardf(kRes2, c);
+            r2 = r2 + (coin > 0 ? (float)coin : 0.5f);
+          }
+          const uint32_t prev = nib_take(H, c);            // Deck::activate's hand part (the active
+          n_in_hand = (n_in_hand - 1u) & 0xffu;            // pile: the drawing wave, trio_drawer)
+          const bool pl = prev > 1u;
+          const uint32_t bp = 1u << (c + 1);              // the play bit; the special bit 23 + c
+          selb.w0 = pl ? (selb.w0 | bp) : (selb.w0 & ~bp);
+          const bool sp = pl && is_special(c);
+          const uint32_t bs0 = c <= 8 ? 1u << (23 + c) : 0u, bs1 = c >= 9 ? 1u << (c - 9) : 0u;
+          selb.w0 = sp ? (selb.w0 | bs0) : (selb.w0 & ~bs0);
+          selb.w1 = sp ? (selb.w1 | bs1) : (selb.w1 & ~bs1);
+          n_active = (n_active + 1u) & 0xffu;
+          pp.z = (pp.z & ~0xffu) | (uint32_t)c;            // idx_last
+        } else {
+          phase = phase == COG_PHASE_BUYING ? COG_PHASE_INACTIVE : phase + 1u;   // pass: next phase
+        }
+        turn_end = phase == COG_PHASE_INACTIVE;            // maybe_end_turn -> next_agent
+        if (turn_end) {
+          n_active = 0u;                                   // Player::end_turn (the deck: drawing wave)
+          stab = selb;                                     // save_actionmask
+          R.set_agent((uint32_t)na);
+          selb = stnb;                                     // load_actionmask (na != ag: >= 3 players)
+          stnb.w2 = (stnb.w2 & ~kMoveShopBits) | 0x204u;   // update_observation, INACTIVE phase
+          r0 = r1 = r2 = 0.f;
+          R.turn_counter++;
+        }
+        R.sh[0] = (R.sh[0] & ~0xffu) | phase;
+        R.sh[1] = __float_as_uint(r0); R.sh[2] = __float_as_uint(r1); R.sh[3] = __float_as_uint(r2);
+        // done (environment.cpp:183-207): the (next) agent's cell or the turn counter
+        const uint2 cc = turn_end ? cells_n : cells_a;
+        const uint32_t c0 = R.use_cell(cc, 0);
+        finish = COG_HEX_END(c0) || R.turn_counter >= R.max_steps;
         if (finish) R.set_done(1u);
-        ended = was_done || finish;
         PH(0);
       }
+      ended = was_done || finish;
     }
     uint4(*ring)[64] = D.ring[sl];
     int ag1 = ag, na1 = na;
@@ -3751,15 +3848,12 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
       na1 = (int)next_player((uint32_t)ag1, R.n_players());
     }
     const bool tc = live && ag1 != ag;                     // turn change: ag1 == na acts next
-    // the new agent's records (hand, counters) and the next player's (stored mask, n_active), once
-    // the drawing wave is past their last turn ends; read ahead of the record's stores, so that
-    // their latency overlaps them
-    uint4 hd1 = make_uint4(0u, 0u, 0u, 0u), hd2 = hd1, pla = hd1, hdn = hd1;
-    uint32_t pln_y = 0u;
+    // the new agent's records (hand, counters) and the next player's (stored mask), once the
+    // drawing wave is past their last turn ends; read ahead of the record's stores, so that their
+    // latency overlaps them
+    uint4 hd = make_uint4(0u, 0u, 0u, 0u), pla = hd, hdn = hd;
     if (__builtin_amdgcn_ballot_w64(tc)) {
-      int need = -1;                                       // the later of ag1's and na1's last turn ends
-#pragma unroll
-      for (int p = 0; p < 4; p++) need = (p == ag1 || p == na1) ? max(need, tend[p]) : need;
+      const int need = R.n_players() == 3u ? te1 : te2;   // the later of ag1's and na1's last turn ends
       // the drawing wave past record max(need) over the wave: its distance from t by ballots (no
       // cross-lane shuffles, which go through LDS); >= 2 in play (>= 3 players, turns of >= 2
       // steps), and from 5 on it asks for a little more than it needs
@@ -3768,26 +3862,25 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
         int dmin = 5;
 #pragma unroll
         for (int d = 4; d >= 1; d--) dmin = __builtin_amdgcn_ballot_w64(w && need >= t - d) ? d : dmin;
+        PH(4);
         cnt_wait(D, cc, cc.draw, (uint32_t)(t - dmin + 1), s_glob);
+        PH(5);
       }
       if (tc) {
-        hd1 = D.img[ag1][1][l];
-        hd2 = D.img[ag1][2][l];
+        hd = D.hand4[ag1][l];
         pla = D.pl[ag1][l];
         hdn = D.heads[na1][l];
-        pln_y = D.pl[na1][l].y;
       }
     }
     if (live) {
       // the acting player's counters: the drawing wave's at its turn end, the epilogue's at a park
-      if (tc || ended) D.pl[ag][l] = pack_player(R.P);
-      const MBits bs = bits_of(R.sel), ba = bits_of(R.sta);
+      if (tc || ended) D.pl[ag][l] = pack_lean_player(pp, n_in_hand, n_active, steps_taken);
       const uint32_t info = (R.info_steps >> (8 * ag)) & 0xffu;
       const uint32_t meta = kMetaValid | (uint32_t)ag << 2 | (uint32_t)na << 4 | (uint32_t)na1 << 6 | info << 8 |
                             (ended ? kMetaEnded : 0u) | (stepped ? kMetaStepped : 0u) | (uint32_t)ag1 << 24;
       ring[0][l] = make_uint4(R.sh[0], R.sh[1], R.sh[2], R.sh[3]);
-      ring[1][l] = make_uint4(bs.w0, bs.w1, bs.w2, meta);
-      ring[2][l] = make_uint4(ba.w0, ba.w1, ba.w2, (uint32_t)act[0] | (R.P.n_active & 0xffu) << 8);
+      ring[1][l] = make_uint4(selb.w0, selb.w1, selb.w2, meta);
+      ring[2][l] = make_uint4(stab.w0, stab.w1, stab.w2, a_play | (n_active & 0xffu) << 8);
       D.srng[sl][l] = srng;
     } else {
       ring[1][l] = make_uint4(0u, 0u, 0u, 0u);             // no record
@@ -3795,22 +3888,24 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     cnt_store(D, CNT_REC, (uint32_t)(t + 1));
     PH(1);
     if (tc) {
-#pragma unroll
-      for (int p = 0; p < 4; p++) tend[p] = p == ag ? t : tend[p];
-      R.d[4] = hd1.x; R.d[5] = hd1.y; R.d[6] = hd1.z; R.d[7] = hd1.w;   // its hand from the drawing
-      R.d[8] = hd2.x; R.d[9] = hd2.y; R.d[10] = hd2.z; R.d[11] = hd2.w; // wave's deck
-      R.P = unpack_player(pla);
-      R.cells_a = R.cells_n;
-      R.sta = R.stn;
-      R.stn = heads_of(mbits_of(hdn));
+      te2 = te1;
+      te1 = t;
+      H.w[0] = hd.x; H.w[1] = hd.y; H.w[2] = hd.z;         // its hand from the drawing wave
+      pp = pla;
+      n_in_hand = (pla.y >> 8) & 0xffu;
+      n_active = (pla.y >> 16) & 0xffu;
+      steps_taken = (pla.z >> 8) & 0xffu;
+      lean_p = lean_player(pla, hd.w);
+      stab = stnb;
+      stnb = mbits_of(hdn);
+      cells_a = cells_n;
       uint2 cn = cells[3];                                 // (selects: no indexed registers)
 #pragma unroll
       for (int p = 2; p >= 0; p--) cn = na1 == p ? cells[p] : cn;
-      R.cells_n = cn;
-      R.na_active = (pln_y >> 16) & 0xffu;
+      cells_n = cn;
     }
     if (live && ended) {                                   // hand the env to k_env_fixup
-      duo_store_env_private<true>(s, i, R);
+      trio_store_private(s, i, R, selb);
       rngs[i] = srng;
       park = (uint32_t)t | (finish ? kParkFinish : 0u);
       live = false;
@@ -3819,14 +3914,14 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     na = na1;
     PH(3);
   }
-  if (live) D.pl[ag][l] = pack_player(R.P);               // (the epilogue's)
+  if (live) D.pl[ag][l] = pack_lean_player(pp, n_in_hand, n_active, steps_taken);   // (the epilogue's)
   cnt_store(D, CNT_REC, (uint32_t)steps + 1u);             // the loop is over (storing wave A's epilogue)
-  cnt_wait(D, cc, cc.fin, 3u, s_glob);                        // the other waves are done
-  PH_FLUSH(s_glob);
+  cnt_wait(D, cc, cc.fin, 3u, s_glob);                     // the other waves are done
+  PH(7);                                                   // the drain (the other waves' last records)
   const uint32_t fl = D.flg[l];                            // their hazard flags
   if (live) {                                              // env-level private state back to HBM
     R.flags |= fl;
-    duo_store_env_private<true>(s, i, R);
+    trio_store_private(s, i, R, selb);
     rngs[i] = srng;
   } else if (l < ne && fl) {                               // a parked env: flags of its last records
     reinterpret_cast<uint32_t *>(s.priv + i)[7] = R.flags | fl;
@@ -3834,6 +3929,8 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
   if (l < ne) s.park[i] = park;
   park_list_push(s_glob, park != kParkNone);
   trio_store_players(D, s, ne);                            // every player's records (cooperative)
+  PH(8);                                                   // the epilogue's stores (issued)
+  PH_FLUSH(s_glob);
 }
 
 // The drawing wave keeps every player's deck (img).  It takes records in pairs r, r + 1 (r even):
@@ -3852,8 +3949,10 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
 #pragma unroll
     for (int p = 0; p < 4; p++) {
       const uint4 *src = reinterpret_cast<const uint4 *>(deck_ptr(s, i, p));
+      uint4 dk[7];
 #pragma unroll
-      for (int k = 0; k < 7; k++) D.img[p][k][l] = src[k];
+      for (int k = 0; k < 7; k++) D.img[p][k][l] = dk[k] = src[k];
+      D.hand4[p][l] = hand_nibbles(dk[1], dk[2]);
     }
     rng = reinterpret_cast<const uint32_t *>(s.priv + i)[0];
   }
@@ -3905,6 +4004,7 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
           dd |= 1u << k;
           D.img[ag][k][l] = dk[k];
         }
+      D.hand4[ag][l] = hand_nibbles(dk[1], dk[2]);         // its hand at its next turn
       dm[0] |= j == 0 ? dd : 0u;
       dm[1] |= j == 1 ? dd : 0u;
     }
@@ -3923,7 +4023,7 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
 
 // The store phase of the trio on two waves: wave A (PART 0) the ObsData shared block and the
 // stored masks -- update_observation's heads of the acting player's when the turn goes on (the
-// lean step leaves them, step_lean) -- and wave B (PART 1) the presampled draws (presample), the
+// lean step leaves them) -- and wave B (PART 1) the presampled draws (presample), the
 // selected-mask record, the Info steps byte, the action, dones / agent_selection and the decks.
 // Each keeps its own images of what it stored last.
 template <int PART>
@@ -3936,7 +4036,7 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
   const bool live = l < epw && wbase + (size_t)l < s_glob.n;
   uint8_t *__restrict__ av = actions_glob + wbase * COG_ACTION_BYTES;
   uint4 shb0 = make_uint4(0u, 0u, 0u, 0u);                 // A: ObsData 16128.. as stored
-  MBits selb = {0u, 0u, 0u}, stb[4];                       // B: selected mask; A: stored masks
+  MBits selb = {0u, 0u, 0u};                               // B: the selected mask as stored
   uint2 cells[4];                                          // A: every player's neighbourhood cache
   uint32_t out = ~0u;                                      // B: dones[i] | agent_selection[i] << 8 as stored
   RegEnv E;                                                // A: update_observation's inputs and flags
@@ -3951,7 +4051,7 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
       const uint4 *pv4 = reinterpret_cast<const uint4 *>(s.priv + i);
 #pragma unroll
       for (int p = 0; p < 4; p++) {
-        stb[p] = mbits_of(s.heads[5 * i + 1 + p]);
+        D.stbA[p][l] = s.heads[5 * i + 1 + p];
         cells[p] = reinterpret_cast<const uint2 *>(pv4 + 8)[p];
       }
       const uint4 g1 = pv4[1];
@@ -4013,34 +4113,31 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
     const bool rec = live && (meta & kMetaValid);
     const int ag = (int)((meta >> 2) & 3u), na = (int)((meta >> 4) & 3u);
     if (rec && PART == 0) {
-      const uint4 g0 = D.ring[sl][0][l], xa = D.ring[sl][2][l];
+      const uint4 g0 = D.ring[sl][0][l], xa = D.ring[sl][2][l], oa = D.stbA[ag][l];
       MBits ba{xa.x, xa.y, xa.z};
-      if ((int)(meta >> 24) == ag && (meta & kMetaStepped)) {   // the turn goes on: update_observation of
-        Heads h = heads_of(ba);                            // ag's stored mask (environment.cpp:252-279)
-        const uint32_t phase = g0.x & 0xffu;
+      if ((int)(meta >> 24) == ag && (meta & kMetaStepped)) {   // the turn goes on: update_observation's
+        const uint32_t phase = g0.x & 0xffu;               // heads of ag's stored mask
         const float r0 = __uint_as_float(g0.y), r1 = __uint_as_float(g0.z), r2 = __uint_as_float(g0.w);
-        const uint32_t n_active = (xa.w >> 8) & 0xffu;
+        const uint32_t n_active = (xa.w >> 8) & 0xffu;     // (environment.cpp:252-279)
         uint2 ca = cells[3];                               // (selects: no indexed registers)
 #pragma unroll
         for (int p = 2; p >= 0; p--) ca = ag == p ? cells[p] : ca;
-        h.move = phase == COG_PHASE_MOVEMENT ? E.move_bits(ca, r0, r1, r2, n_active) : 1u;
-        h.shop = phase == COG_PHASE_BUYING ? E.shop_bits(r2) : 1u;
-        ba = bits_of(h);
+        const uint32_t mv = phase == COG_PHASE_MOVEMENT ? E.move_bits(ca, r0, r1, r2, n_active) : 1u;
+        const uint32_t sp = phase == COG_PHASE_BUYING ? E.shop_bits(r2) : 1u;
+        ba.w2 = (ba.w2 & ~kMoveShopBits) | mv << 2 | sp << 9;
       }
       uint8_t *ob = s.obs + i * COG_OBS_BYTES;
       if (ne4(g0, shb0)) reinterpret_cast<uint4 *>(ob + COG_OBS_PHASE)[0] = g0;
       shb0 = g0;
       uint8_t *deck = deck_ptr(s, i, ag);
-      store_mask_record(reinterpret_cast<uint4 *>(deck + COG_PD_MASK), ba, mask_diff_granules(ba, selm(stb, ag)));
-      setm(stb, ag, ba);
+      store_mask_record(reinterpret_cast<uint4 *>(deck + COG_PD_MASK), ba, mask_diff_granules(ba, mbits_of(oa)));
+      D.stbA[ag][l] = mbits_u4(ba);
       if ((int)(meta >> 24) != ag && (meta & kMetaStepped)) {   // a turn end: the new agent's stored mask
-        Heads hn = heads_of(selm(stb, na));                // gets update_observation's INACTIVE-phase
-        hn.move = 1u;                                      // heads (step_lean)
-        hn.shop = 1u;
-        const MBits bn = bits_of(hn);
+        const uint4 on = D.stbA[na][l];                    // gets update_observation's INACTIVE-phase
+        const MBits bn{on.x, on.y, (on.z & ~kMoveShopBits) | 0x204u};   // heads (the lean step)
         store_mask_record(reinterpret_cast<uint4 *>(deck_ptr(s, i, na) + COG_PD_MASK), bn,
-                          mask_diff_granules(bn, selm(stb, na)));
-        setm(stb, na, bn);
+                          mask_diff_granules(bn, mbits_of(on)));
+        D.stbA[na][l] = mbits_u4(bn);
       }
     }
     if (rec && PART == 1) {                                // deck granules the record changed, from img
@@ -4059,7 +4156,7 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
     cnt_wait(D, cc, cc.rec, (uint32_t)steps + 1u, s_glob);
     if (live) {
 #pragma unroll
-      for (int p = 0; p < 4; p++) D.heads[p][l] = mbits_u4(stb[p]);
+      for (int p = 0; p < 4; p++) D.heads[p][l] = D.stbA[p][l];
     }
   }
   PH_FLUSH(s_glob);

@@ -70,7 +70,7 @@ int main(int argc, char **argv) {
       if (hipMalloc(&d, waves * K * sizeof(unsigned long long)) != hipSuccess) return 1;
       if (hipMemset(d, 0, waves * K * sizeof(unsigned long long)) != hipSuccess) return 1;
       env->sh[0].s.stamps = d;
-      const int chunk = 200;
+      const int chunk = getenv("PROBE_CHUNK") ? atoi(getenv("PROBE_CHUNK")) : 200;
       cog_runner_set_chunk(run, chunk);
       cog_runner_rollout(run, chunk);
       cog_runner_sync(run);
@@ -84,9 +84,30 @@ int main(int argc, char **argv) {
                                      "", "", "stores", "", ""};
       const char *draw_names[16] = {"", "", "", "", "", "", "", "", "wait X, Y", "turn-end draws", "", "", "", "", "",
                                     ""};
+      // the trio's stepping wave (trio_stepper): 2 = the loop top's waits (ring slot, presampled
+      // draws), 5 = the turn change's wait for the drawing wave; the rest is its own work
+      const char *trio_step_names[16] = {"sample + lean step", "record + turn-change reads", "wait: slot / draws",
+                                         "turn change", "turn-change distance", "wait: drawing wave",
+                                         "prologue (per launch)", "drain (per launch)", "epilogue (per launch)", "",
+                                         "", "", "", "", "", ""};
       const char *role_name[4] = {"stepping", wpg == 4 ? "drawing" : "storing", "storing A", "storing B"};
+      if (getenv("PROBE_JSON") && wpg == 4) {              // one line for tools/r05/stamps_profile.py
+        double ph[16];
+        for (int k = 0; k < 16; k++) {
+          std::vector<double> v;
+          for (size_t w = 0; w < waves; w += wpg) v.push_back((double)h[w * K + k] / chunk);
+          ph[k] = med(v);
+        }
+        const double wait = ph[2] + ph[5], busy = ph[0] + ph[1] + ph[3] + ph[4];
+        printf("STAMPS_JSON {\"envs\": %zu, \"steps_per_launch\": %d, \"busy_ticks_per_step\": %.1f, "
+               "\"wait_ticks_per_step\": %.1f, \"ticks_per_step\": %.1f, \"busy_frac\": %.4f, \"phases\": {",
+               n, chunk, busy, wait, busy + wait, busy / (busy + wait));
+        for (int k = 0; k < 9; k++) printf("%s\"%s\": %.1f", k ? ", " : "", trio_step_names[k], ph[k]);
+        printf("}}\n");
+      }
       for (int role = 0; role < wpg; role++) {
-        const char **pn = role == 0 ? step_names : (wpg == 4 && role == 1) ? draw_names : store_names;
+        const char **pn = role == 0 ? (wpg == 4 ? trio_step_names : step_names)
+                                    : (wpg == 4 && role == 1) ? draw_names : store_names;
         double tot = 0;
         printf("  %s wave:\n", role_name[role]);
         for (int k = 0; k < 16; k++) {
