@@ -3515,26 +3515,29 @@ constexpr int kTrioRingG = 3;
 #endif
 constexpr int kTrioDepth = COG_TRIO_DEPTH;                 // ring slots (records in flight)
 constexpr int kTrioLead = 4;                               // presampled draws: steps ahead of the record
-constexpr int kTrioBLag = 2;                               // storing wave B: deck cursor behind its front
+#ifndef COG_TRIO_BLAG                                      // (diagnostic A/B builds)
+#define COG_TRIO_BLAG 2
+#endif
+constexpr int kTrioBLag = COG_TRIO_BLAG;                   // storing wave B: deck cursor behind its front
 // CNT_ABORT: set (sticky) by the first progress wait that times out; every later wait of every
 // wave returns at once, so a broken invariant ends the launch promptly with the error set
 // (instead of one ~0.2 s timeout per remaining wait)
 enum TrioCnt : int { CNT_REC = 0, CNT_DRAW, CNT_STA, CNT_STB, CNT_PRE, CNT_FIN, CNT_ABORT, kTrioCnts };
 constexpr uint32_t kTrioSpinLimit = 1u << 21;             // polls (~0.2 s)
 struct TrioLds {
-  uint4 img[4][7][64];                // every player's DeckObs (the drawing wave's)
+  uint2 img[4][5][64];                // every player's compact DeckObs (the drawing wave's): piles of types 0-7
   uint4 ring[kTrioDepth][kTrioRingG][64];   // record t (above), t % 8
   uint32_t srng[kTrioDepth][64];      // the sampler state after step t, t % 8
   uint3 pre[kTrioLead][64];           // step t's presampled draws, t % 4: state, head 0's draw | risk << 31, state after
   uint4 pl[4][64];
   uint4 heads[4][64];
-  uint4 hand4[4][64];                 // every player's hand as nibbles (hand_nibbles: the drawing wave's)
   uint4 stbA[4][64];                  // storing wave A: every player's stored mask as last stored (bits)
+  uint32_t wide[64];                  // the env's deck holds a type >= 8 (the drawing wave's prologue)
   uint32_t flg[64];                   // the other waves' hazard flags (the stepping wave's epilogue)
   uint32_t cnt[kTrioCnts];            // progress counters
   UidEntry tab[kUidTab];
 };
-static_assert(sizeof(TrioLds) <= 75520, "two trio workgroups per CU (measured: 78,336 B admit one)");
+static_assert(sizeof(TrioLds) <= 54613, "three trio workgroups per CU");
 static_assert((kTrioDepth & (kTrioDepth - 1)) == 0 && kTrioDepth >= 4, "ring slots: a power of two");
 
 // A wave keeps the counters it last read (wave-uniform, in SGPRs) and reads them again -- all six
@@ -3604,48 +3607,62 @@ DEV void trio_store_players(const TrioLds &D, const DevState &s, int ne) {
   }
 }
 
-// ---- the stepping wave's lean image (round 5) ----------------------------------------------
-// The acting player's hand as 4-bit counts (nibble c = hand[c], types 0-7 / 8-15 / 16-20 in three
-// dwords), made by the drawing wave from its deck image (hand_nibbles: at the prologue and after
-// each turn end's draws) with a flag when a count exceeds 15; the player record packed, with the
-// three counters the lean step changes unpacked; the masks as bit vectors (MBits).  A play reads
-// and decrements one nibble instead of selecting over the six dwords of the byte pile.
-struct LeanHand {
-  uint32_t w[3];
-};
-// the drawing wave: hand[0..20] of a DeckObs image (bytes 21..41) as nibbles; .w = 1 when a count
-// does not fit a nibble (the stepping wave then parks the player's steps: kParkRedo)
-DEV uint4 hand_nibbles(const uint4 g1, const uint4 g2) {
-  const uint32_t d[8] = {g1.x, g1.y, g1.z, g1.w, g2.x, g2.y, g2.z, g2.w};   // deck bytes 16..47
-  uint32_t h[6], ovf = 0u;
+// ---- the stepping wave's lean image and the compact deck (round 5) ----------------------------
+// Decks in LDS hold types 0-7 only ("narrow": the canonical loop's decks never hold another type --
+// no purchases, no specials -- DeckObs piles draw / hand / active / played / discard, 8 counts
+// each, a uint2 per pile): 160 B per env instead of 448, so that four workgroups fit a CU's LDS and
+// the metric's 65,536 envs step in one round.  An env whose deck holds a type >= 8 (compact_of
+// says wide) is parked at step 0 and run by k_env_fixup's full step.  The acting player's hand is
+// the stepping wave's copy of its compact hand pile (two dwords of u8 counts).
+// DeckObs byte offset of pile p (api.h:67-82): 21 p
+DEV void deck_expand(const uint2 pile[5], uint4 dk[7]) {   // compact -> the record's 7 granules
+  uint32_t d[28];
 #pragma unroll
-  for (int q = 0; q < 6; q++) {                            // hand bytes 4q..4q+3 (byte 21 + 4q = deck
-    uint32_t x = fsh8(d[q + 2], d[q + 1], 1);              // dword 5 + q, byte 1)
-    if (q == 5) x &= 0xffu;                                // hand[20] only (then the active pile)
-    ovf |= x & 0xf0f0f0f0u;
-    h[q] = x;
-  }
-  uint32_t w[3];
+  for (int k = 0; k < 28; k++) d[k] = 0u;
 #pragma unroll
-  for (int k = 0; k < 3; k++) {                            // 8 counts per dword
-    const uint32_t lo = h[2 * k], hi = 2 * k + 1 < 6 ? h[2 * k + 1] : 0u;
-    const uint32_t a = (lo | (lo >> 4)) & 0x00ff00ffu, b = (hi | (hi >> 4)) & 0x00ff00ffu;
-    w[k] = ((a | (a >> 8)) & 0xffffu) | ((b | (b >> 8)) & 0xffffu) << 16;
+  for (int p = 0; p < 5; p++) {
+    const int b = 21 * p, q = b >> 2, sh = b & 3;          // compile-time
+    const uint32_t lo = pile[p].x, hi = pile[p].y;
+    if (sh == 0) {
+      d[q] |= lo;
+      d[q + 1] |= hi;
+    } else {
+      d[q] |= lo << (8 * sh);
+      d[q + 1] |= __builtin_amdgcn_alignbyte(hi, lo, 4 - sh);
+      d[q + 2] |= hi >> (8 * (4 - sh));
+    }
   }
-  return make_uint4(w[0], w[1], w[2], ovf ? 1u : 0u);
+#pragma unroll
+  for (int k = 0; k < 7; k++) dk[k] = make_uint4(d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]);
 }
-// card c leaves the hand (Deck::activate's hand part, player.cpp:45-60, cards.cpp:242-253): the
-// count before (a count of 0 stays 0 here -- the reference wraps it to 255 (u8), the drawing wave's
-// byte image too, but the play bit of c is then clear and no lean step plays c again before the
-// drawing wave's next hand_nibbles, which flags the 255)
-DEV uint32_t nib_take(LeanHand &H, int c) {
-  const int q = c >> 3, sh = 4 * (c & 7);
-  const uint32_t w = q == 0 ? H.w[0] : (q == 1 ? H.w[1] : H.w[2]);
-  const uint32_t prev = (w >> sh) & 0xfu;
-  const uint32_t nw = w - ((prev ? 1u : 0u) << sh);
-  H.w[0] = q == 0 ? nw : H.w[0];
-  H.w[1] = q == 1 ? nw : H.w[1];
-  H.w[2] = q == 2 ? nw : H.w[2];
+// the record's granules -> compact piles; false: a count of a type >= 8 is non-zero (wide)
+DEV bool compact_of(const uint4 dk[7], uint2 pile[5]) {
+  uint32_t d[28];
+#pragma unroll
+  for (int k = 0; k < 7; k++) { d[4 * k] = dk[k].x; d[4 * k + 1] = dk[k].y; d[4 * k + 2] = dk[k].z; d[4 * k + 3] = dk[k].w; }
+  uint32_t rest = 0u;                                      // every byte of types 8..20
+#pragma unroll
+  for (int p = 0; p < 5; p++) {
+    const int b = 21 * p, q = b >> 2, sh = b & 3;
+    pile[p].x = sh ? __builtin_amdgcn_alignbyte(d[q + 1], d[q], sh) : d[q];
+    pile[p].y = sh ? __builtin_amdgcn_alignbyte(d[q + 2], d[q + 1], sh) : d[q + 1];
+#pragma unroll
+    for (int t = 8; t < 21; t++) {                         // bytes b + 8 .. b + 20
+      const int y = b + t;
+      rest |= (d[y >> 2] >> (8 * (y & 3))) & 0xffu;
+    }
+  }
+  return rest == 0u;
+}
+// card c (< 8) leaves the compact hand (Deck::activate's hand part, player.cpp:45-60,
+// cards.cpp:242-253: hand[c] - 1, u8): the count before
+DEV uint32_t hand_take(uint2 &h, int c) {
+  const uint32_t sh = 8u * (uint32_t)(c & 3);
+  const uint32_t w = c < 4 ? h.x : h.y;
+  const uint32_t prev = (w >> sh) & 0xffu;
+  const uint32_t nw = (w & ~(0xffu << sh)) | (((prev - 1u) & 0xffu) << sh);
+  h.x = c < 4 ? nw : h.x;
+  h.y = c < 4 ? h.y : nw;
   return prev;
 }
 // the selected mask's heads 1-4 are {0} (special, remove, move, shop: MBits bits 22.., w1, w2)
@@ -3680,8 +3697,8 @@ DEV uint4 pack_lean_player(uint4 pp, uint32_t n_in_hand, uint32_t n_active, uint
 }
 // the lean step may run for this player: no move, free card, free move or pending removes in
 // progress, has not won (PlayerPriv x: has_won, mip, n_removes, next_card_free; y byte 0:
-// next_move_free), and its hand counts fit the nibbles
-DEV bool lean_player(const uint4 &pp, uint32_t hand_ovf) { return (pp.x | (pp.y & 0xffu) | hand_ovf) == 0u; }
+// next_move_free)
+DEV bool lean_player(const uint4 &pp) { return (pp.x | (pp.y & 0xffu)) == 0u; }
 // the env-level private records from the stepping wave (duo_store_env_private<true> with the
 // selected mask as bits)
 DEV void trio_store_private(const DevState &s, size_t i, const RegEnv &R, const MBits &selb) {
@@ -3748,12 +3765,12 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
   R.tab = D.tab;
   __builtin_amdgcn_s_waitcnt(0);                           // (no per-iteration vmcnt wait covers them)
   __syncthreads();                                         // B: every wave's prologue is done
-  LeanHand H = {{0u, 0u, 0u}};
-  bool lean_p = false;
-  if (live) {                                              // ag's hand: the drawing wave's nibbles
-    const uint4 h4 = D.hand4[ag][l];
-    H.w[0] = h4.x; H.w[1] = h4.y; H.w[2] = h4.z;
-    lean_p = lean_player(pp, h4.w);
+  uint2 H = make_uint2(0u, 0u);                            // ag's hand (compact: types 0-7)
+  bool lean_p = false, narrow = false;
+  if (live) {                                              // from the drawing wave's image
+    H = D.img[ag][1][l];
+    narrow = D.wide[l] == 0u;
+    lean_p = narrow && lean_player(pp);
   }
   PH(6);                                                   // the prologue (to the barrier)
   TrioCnt6 cc;
@@ -3763,6 +3780,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
       cnt_wait(D, cc, cc.sta, (uint32_t)(t - kTrioDepth + 1), s_glob);
       cnt_wait(D, cc, cc.stb, (uint32_t)(t - kTrioDepth + 1), s_glob);
     }
+    PH(9);
     if (t >= kTrioLead) cnt_wait(D, cc, cc.pre, (uint32_t)(t - kTrioLead + 1), s_glob);
     PH(2);
     bool ended = false, finish = false, turn_end = false, stepped = false;
@@ -3779,6 +3797,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
         a_play = act[0];
         other = ((uint32_t)act[1] | act[2] | act[3] | act[4]) != 0u;
       }
+      other = other || a_play > 8u;                        // (a type >= 8: not in a narrow deck's hand)
       const bool was_done = R.done() != 0u;
       // not the lean step's case (never in the canonical loop), or the test hook: hand the env to
       // k_env_fixup before its step t
@@ -3797,7 +3816,6 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
         if (phase == COG_PHASE_INACTIVE) phase = COG_PHASE_MOVEMENT;
         steps_taken = (steps_taken + 1u) & 0xffu;
         float r0 = __uint_as_float(R.sh[1]), r1 = __uint_as_float(R.sh[2]), r2 = __uint_as_float(R.sh[3]);
-        if (a_play > 8u) pp.z = (pp.z & 0x00ffffffu) | 0x01000000u;   // the deck's "wide" flag (step_regs)
         if (a_play) {                                      // Player::play_card (player.cpp:45-60)
           const int c = (int)a_play - 1;
           if (phase == COG_PHASE_MOVEMENT) {
@@ -3806,7 +3824,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
             const uint32_t coin = cardf(kRes2, c);
             r2 = r2 + (coin > 0 ? (float)coin : 0.5f);
           }
-          const uint32_t prev = nib_take(H, c);            // Deck::activate's hand part (the active
+          const uint32_t prev = hand_take(H, c);           // Deck::activate's hand part (the active
           n_in_hand = (n_in_hand - 1u) & 0xffu;            // pile: the drawing wave, trio_drawer)
           const bool pl = prev > 1u;
           const uint32_t bp = 1u << (c + 1);              // the play bit; the special bit 23 + c
@@ -3851,7 +3869,8 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     // the new agent's records (hand, counters) and the next player's (stored mask), once the
     // drawing wave is past their last turn ends; read ahead of the record's stores, so that their
     // latency overlaps them
-    uint4 hd = make_uint4(0u, 0u, 0u, 0u), pla = hd, hdn = hd;
+    uint2 hd = make_uint2(0u, 0u);
+    uint4 pla = make_uint4(0u, 0u, 0u, 0u), hdn = pla;
     if (__builtin_amdgcn_ballot_w64(tc)) {
       const int need = R.n_players() == 3u ? te1 : te2;   // the later of ag1's and na1's last turn ends
       // the drawing wave past record max(need) over the wave: its distance from t by ballots (no
@@ -3867,7 +3886,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
         PH(5);
       }
       if (tc) {
-        hd = D.hand4[ag1][l];
+        hd = D.img[ag1][1][l];
         pla = D.pl[ag1][l];
         hdn = D.heads[na1][l];
       }
@@ -3890,12 +3909,12 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     if (tc) {
       te2 = te1;
       te1 = t;
-      H.w[0] = hd.x; H.w[1] = hd.y; H.w[2] = hd.z;         // its hand from the drawing wave
+      H = hd;                                              // its hand from the drawing wave
       pp = pla;
       n_in_hand = (pla.y >> 8) & 0xffu;
       n_active = (pla.y >> 16) & 0xffu;
       steps_taken = (pla.z >> 8) & 0xffu;
-      lean_p = lean_player(pla, hd.w);
+      lean_p = narrow && lean_player(pla);
       stab = stnb;
       stnb = mbits_of(hdn);
       cells_a = cells_n;
@@ -3945,17 +3964,22 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
   const size_t i = (size_t)l;
   const bool live = l < epw && wbase + (size_t)l < s_glob.n;
   uint32_t rng = 0u;                                       // the env rng
+  bool narrow = true;
   if (live) {
 #pragma unroll
     for (int p = 0; p < 4; p++) {
       const uint4 *src = reinterpret_cast<const uint4 *>(deck_ptr(s, i, p));
       uint4 dk[7];
+      uint2 pile[5];
 #pragma unroll
-      for (int k = 0; k < 7; k++) D.img[p][k][l] = dk[k] = src[k];
-      D.hand4[p][l] = hand_nibbles(dk[1], dk[2]);
+      for (int k = 0; k < 7; k++) dk[k] = src[k];
+      narrow = compact_of(dk, pile) && narrow;
+#pragma unroll
+      for (int q = 0; q < 5; q++) D.img[p][q][l] = pile[q];
     }
     rng = reinterpret_cast<const uint32_t *>(s.priv + i)[0];
   }
+  D.wide[l] = narrow ? 0u : 1u;                            // (a wide env: the stepper parks it at step 0)
   uint32_t flags = 0u;                                     // hazard flags of the draws
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();                                         // B: the decks are in LDS
@@ -3979,32 +4003,35 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
       te[j] = rec && (int)(meta >> 24) != ag;
       const int a_play = (int)(D.ring[slot[j]][2][l].w & 0xffu);
       if (rec && a_play) {                                 // Deck::activate (cards.cpp:242-253): hand[c]--,
-        const int bh = COG_DECK_HAND + a_play - 1, ba = COG_DECK_ACTIVE + a_play - 1;   // active[c]++ (u8)
-        uint8_t *ph = reinterpret_cast<uint8_t *>(&D.img[ag][bh >> 4][l]) + (bh & 15);
-        uint8_t *pa = reinterpret_cast<uint8_t *>(&D.img[ag][ba >> 4][l]) + (ba & 15);
+        const int c = a_play - 1;                          // active[c]++ (u8; c < 8: the stepping wave
+        uint8_t *ph = reinterpret_cast<uint8_t *>(&D.img[ag][1][l]) + c;   // parks any other type)
+        uint8_t *pa = reinterpret_cast<uint8_t *>(&D.img[ag][2][l]) + c;
         *ph = (uint8_t)(*ph - 1u);
         *pa = (uint8_t)(*pa + 1u);
+        const int bh = COG_DECK_HAND + c, ba = COG_DECK_ACTIVE + c;   // the record's granules
         dm[j] |= 1u << (bh >> 4) | 1u << (ba >> 4);
       }
     }
     const bool any = te[0] || te[1];                       // (at most one of them)
     if (__builtin_amdgcn_ballot_w64(any) && any) {         // the turn end's discard + draws
       const int j = te[1] ? 1 : 0, sl = te[1] ? slot[1] : slot[0], ag = te[1] ? agj[1] : agj[0];
-      uint4 dk[7], old[7];
+      uint2 pile[5];
 #pragma unroll
-      for (int k = 0; k < 7; k++) old[k] = dk[k] = D.img[ag][k][l];
+      for (int q = 0; q < 5; q++) pile[q] = D.img[ag][q][l];
+      uint4 dk[7], old[7];
+      deck_expand(pile, dk);
+#pragma unroll
+      for (int k = 0; k < 7; k++) old[k] = dk[k];
       const uint4 x = D.ring[sl][2][l];
       MBits ba{x.x, x.y, x.z};
-      duo_turn_end(D, l, ag, dk, ba, rng, flags);
+      duo_turn_end(D, l, ag, dk, ba, rng, flags);          // (a narrow deck stays narrow)
       D.ring[sl][2][l] = make_uint4(ba.w0, ba.w1, ba.w2, x.w);
       uint32_t dd = 0;
 #pragma unroll
-      for (int k = 0; k < 7; k++)
-        if (ne4(dk[k], old[k])) {
-          dd |= 1u << k;
-          D.img[ag][k][l] = dk[k];
-        }
-      D.hand4[ag][l] = hand_nibbles(dk[1], dk[2]);         // its hand at its next turn
+      for (int k = 0; k < 7; k++) dd |= ne4(dk[k], old[k]) ? 1u << k : 0u;
+      (void)compact_of(dk, pile);
+#pragma unroll
+      for (int q = 0; q < 5; q++) D.img[ag][q][l] = pile[q];
       dm[0] |= j == 0 ? dd : 0u;
       dm[1] |= j == 1 ? dd : 0u;
     }
@@ -4104,6 +4131,7 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
         }
       }
     }
+    PH(7);
     const int q = r - LAG;                                 // record q drawn
     if (q < 0) continue;                                   // (uniform)
     const int sl = q & (kTrioDepth - 1);
@@ -4142,10 +4170,15 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
     }
     if (rec && PART == 1) {                                // deck granules the record changed, from img
       const uint32_t dm = D.ring[sl][2][l].w >> 16;
+      uint2 pile[5];
+#pragma unroll
+      for (int q = 0; q < 5; q++) pile[q] = D.img[ag][q][l];
+      uint4 dk[7];
+      deck_expand(pile, dk);
       uint4 *deck = reinterpret_cast<uint4 *>(deck_ptr(s, i, ag));
 #pragma unroll
       for (int k = 0; k < 7; k++)
-        if ((dm >> k) & 1u) deck[k] = D.img[ag][k][l];
+        if ((dm >> k) & 1u) deck[k] = dk[k];
     }
     cnt_store(D, PART == 0 ? CNT_STA : CNT_STB, (uint32_t)(q + 1));
     PH(13);
@@ -4168,7 +4201,7 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
 // waves leave their hazard flags in flg[] and count themselves done in cnt[FIN]; the stepping wave
 // waits for all three before its epilogue.
 template <int SRC>
-__global__ void __launch_bounds__(256) k_env_rollout_trio(DevState s, int steps, int epw, uint32_t *__restrict__ rngs,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_env_rollout_trio(DevState s, int steps, int epw, uint32_t *__restrict__ rngs,
                                                           uint8_t *__restrict__ actions_out) {
   __shared__ TrioLds D;
   // (roles rotated per workgroup, so that a CU's two workgroups could not put both stepping waves
@@ -4521,6 +4554,23 @@ int trio_epw(size_t n) {
   (void)n;
   return 64;
 }
+// Trio workgroups per CU.  The compact decks (TrioLds, 53 KB) admit three per CU, but the output
+// stores are bound by each XCD's L2: at 65,536 envs, 32,768 stepping at once keep an XCD's written
+// lines (~4.7 per env-step) within its 4 MiB L2, 49,152 or all 65,536 do not (measured: four per
+// CU, all 65,536 at once, 3.94 us per step; three per CU 4.01; two per CU, in two rounds, 2.75;
+// one per CU 5.43: profiles/r05f_trio_wpc.txt).  So a launch of more than one workgroup per CU
+// pads each workgroup's LDS to half a CU's (the dispatcher would otherwise pack three on some CUs);
+// $COG_TRIO_WPC = 1..4 overrides (A/B).
+static size_t trio_pad_lds(unsigned nblocks) {
+  static const int forced = [] {
+    const char *e = getenv("COG_TRIO_WPC");
+    return e && *e ? atoi(e) : 0;
+  }();
+  const int wpc = forced >= 1 && forced <= 4 ? forced : (nblocks > 256u ? 2 : 0);
+  if (!wpc) return 0;
+  const size_t per = (size_t)163840 / (size_t)wpc - 2048;  // (a margin for the allocation granule)
+  return per > sizeof(TrioLds) ? per - sizeof(TrioLds) : 0;
+}
 // k_env_fixup's grid: at most this many one-wave workgroups stride over the parked list
 // ($COG_FIXUP_GRID overrides; A/B only).  A wave per CU keeps a launch with every workgroup parked
 // (short episodes) running in parallel, and a launch with none parked cheap.
@@ -4556,7 +4606,8 @@ int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rn
       // (k_env_fixup inside the trio launch, for shards of one workgroup per CU -- inlined, or as a
       // never-inlined call -- was slower: 20-step launch at 8,192 44.2 / 42.0 against 41.3 us,
       // profiles/r04t_trio_fused.txt)
-      hipLaunchKernelGGL((k_env_rollout_trio<MASK_SELECTED>), g, dim3(256), 0, st, sd, steps, epw, d_rng, d_actions);
+      hipLaunchKernelGGL((k_env_rollout_trio<MASK_SELECTED>), g, dim3(256), trio_pad_lds(nb), st, sd, steps, epw, d_rng,
+                         d_actions);
       hipLaunchKernelGGL((k_env_fixup<MASK_SELECTED>), gf, dim3(64), 0, st, sd, steps, d_rng, d_actions, epw);
     } else {
       hipLaunchKernelGGL((k_env_rollout_duo<MASK_SELECTED>), g, dim3(128), 0, st, sd, steps, d_rng, d_actions);

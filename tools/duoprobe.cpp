@@ -80,15 +80,16 @@ int main(int argc, char **argv) {
       const char *step_names[16] = {"step tail (done check)", "LDS player writes", "wait X", "ring write + turn change",
                                     "wait Y", "", "", "", "sample + action branch", "mip + end_turn discard",
                                     "draw", "mask swap, sh, cells", "update_observation", "", "", ""};
-      const char *store_names[16] = {"", "", "", "", "", "wait Y", "ring read, images, slot", "wait X", "", "", "",
-                                     "", "", "stores", "", ""};
-      const char *draw_names[16] = {"", "", "", "", "", "", "", "", "wait X, Y", "turn-end draws", "", "", "", "", "",
-                                    ""};
+      const char *store_names[16] = {"", "", "", "", "", "wait Y / B: wait record", "A: wait drawn / B: wait drawn",
+                                     "wait X / B: front cursor work", "", "", "", "", "", "stores (the drawn record's)",
+                                     "", ""};
+      const char *draw_names[16] = {"", "", "", "", "", "", "", "", "wait: records", "plays + turn-end draws", "", "", "",
+                                    "", "", ""};
       // the trio's stepping wave (trio_stepper): 2 = the loop top's waits (ring slot, presampled
       // draws), 5 = the turn change's wait for the drawing wave; the rest is its own work
-      const char *trio_step_names[16] = {"sample + lean step", "record + turn-change reads", "wait: slot / draws",
+      const char *trio_step_names[16] = {"sample + lean step", "record + turn-change reads", "wait: presampled draws",
                                          "turn change", "turn-change distance", "wait: drawing wave",
-                                         "prologue (per launch)", "drain (per launch)", "epilogue (per launch)", "",
+                                         "prologue (per launch)", "drain (per launch)", "epilogue (per launch)", "wait: ring slot",
                                          "", "", "", "", "", ""};
       const char *role_name[4] = {"stepping", wpg == 4 ? "drawing" : "storing", "storing A", "storing B"};
       if (getenv("PROBE_JSON") && wpg == 4) {              // one line for tools/r05/stamps_profile.py
@@ -98,11 +99,11 @@ int main(int argc, char **argv) {
           for (size_t w = 0; w < waves; w += wpg) v.push_back((double)h[w * K + k] / chunk);
           ph[k] = med(v);
         }
-        const double wait = ph[2] + ph[5], busy = ph[0] + ph[1] + ph[3] + ph[4];
+        const double wait = ph[2] + ph[5] + ph[9], busy = ph[0] + ph[1] + ph[3] + ph[4];
         printf("STAMPS_JSON {\"envs\": %zu, \"steps_per_launch\": %d, \"busy_ticks_per_step\": %.1f, "
                "\"wait_ticks_per_step\": %.1f, \"ticks_per_step\": %.1f, \"busy_frac\": %.4f, \"phases\": {",
                n, chunk, busy, wait, busy + wait, busy / (busy + wait));
-        for (int k = 0; k < 9; k++) printf("%s\"%s\": %.1f", k ? ", " : "", trio_step_names[k], ph[k]);
+        for (int k = 0; k < 10; k++) printf("%s\"%s\": %.1f", k ? ", " : "", trio_step_names[k], ph[k]);
         printf("}}\n");
       }
       for (int role = 0; role < wpg; role++) {

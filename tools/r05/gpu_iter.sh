@@ -9,6 +9,10 @@ mkdir -p "$OUT"
 K=${2:-"trio or timed or rollout or golden or configs or horizon or views or parity"}
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "$K" > "$OUT/tests.log" 2>&1 && \
 PROBE_SHORT=1 timeout -k 10 120 tools/r05/bin/duoprobe trio 65536 8192 > "$OUT/probe.txt" 2>&1 && \
+for v in tools/r05/bin/duoprobe_v*; do
+  [ -x "$v" ] || continue
+  timeout -k 10 120 "$v" "$(basename "$v")" 65536 8192 >> "$OUT/probe.txt" 2>&1 || exit 1
+done && \
 PROBE_JSON=1 timeout -k 10 120 tools/r05/bin/duoprobe_st trio 65536 8192 > "$OUT/stamps.txt" 2>&1 && \
 PROBE_JSON=1 PROBE_CHUNK=20 timeout -k 10 120 tools/r05/bin/duoprobe_st trio 65536 8192 > "$OUT/stamps20.txt" 2>&1
 rc=$?
