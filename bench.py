@@ -469,7 +469,6 @@ def roofline(prof, n, k_chunk, launch_s, kind="trio", stamps=None):
         out["achieved"] = tr / launch_s / 1e9
         out["frac"] = tr / launch_s / 1e9 / HBM_PEAK_GBS
         out["counter_bytes_per_env_step"] = tr / n / k_chunk
-        out["pmc_kernel_ns"] = e.get("kernel_ns")
     st = ((stamps or {}).get("shapes") or {}).get(str(n))
     if st:
         out["limiter"].update({k: st[k] for k in ("busy_ticks_per_step", "wait_ticks_per_step", "ticks_per_step",

@@ -281,11 +281,20 @@ struct EnvShard {
   bool host_synced = false, pub_done = false;
   Signal done;                        // completion word: word 32 of the shard's error line
   uint32_t park_seq = 0;              // rollout launches with a fix-up so far (DevState::park_par)
+  // Steps since the last reset during which only trio rollouts ran (kNotLean: something else ran,
+  // or the shard was never reset with >= 3 players).  After a reset every player is lean (no move,
+  // free card / move or removes in progress, narrow decks, nobody has won), the selected-mask loop
+  // keeps them so -- no moves, purchases or specials -- and the turn counter grows by at most one
+  // per step, so no env of the shard can park before lean_clock + K >= max_steps: a trio launch of
+  // K steps then needs no k_env_fixup (cog::launch_rollout's no_fixup; the kernel reports a park
+  // anyway as an error, F_PARK_NOFIX).
+  uint64_t lean_clock = ~0ull;
 };
 
 struct cog_env {
   size_t n = 0;
   uint8_t n_players = 4;              // the batch's players (reset params; the default ctor's 4)
+  uint32_t max_steps = 0;             // the last reset's max_steps (0: unknown)
   std::vector<EnvShard> sh;
   uint32_t *h_err = nullptr;          // pinned, device-mapped: one error word per shard (256 B apart)
   // host views: obs is one pinned allocation; the small records are the shard's h_outs block
@@ -414,6 +423,8 @@ int status_to_rc(uint32_t flags, uint32_t errors) {
   if (errors) {
     if (flags & cog::F_SYNC_TIMEOUT)
       return fail(COG_ERR_HIP, "internal error: a rollout wave's progress wait timed out (outputs invalid)");
+    if (flags & cog::F_PARK_NOFIX)
+      return fail(COG_ERR_HIP, "internal error: an env parked in a rollout launched without its fix-up (outputs invalid)");
     if (flags & cog::F_GRID_OVER)
       return fail(COG_ERR_MAPGEN, "map generation produced a map larger than the 48x48 observation grid");
     return fail(COG_ERR_MAPGEN, "Failed to generate map in specified maximum number of attempts");
@@ -734,10 +745,14 @@ int cog_env_shard_info(const cog_env *env, int k, size_t *first, size_t *count, 
 static int env_reset_impl(cog_env *e, const cog::ResetParams &p) {
   int rc = prepare_host(e);
   if (rc) return rc;
-  if (p.use_params) e->n_players = p.n_players;
+  if (p.use_params) {
+    e->n_players = p.n_players;
+    e->max_steps = p.max_steps;
+  }
   for (EnvShard &k : e->sh) {
     k.done.queued = false;
     k.host_synced = false;                                 // (refresh_full: the mirror is rebuilt later)
+    k.lean_clock = e->n_players >= 3 && e->max_steps ? 0ull : ~0ull;
   }
   for (EnvShard &k : e->sh) {
     DeviceGuard g(k.device);
@@ -791,6 +806,7 @@ int cog_env_step_device_stream(cog_env *env, const void *d_actions, size_t n, vo
     HIPCHK(hipEventRecord(k.ev, static_cast<hipStream_t>(stream)));   // (NULL: the null stream)
     HIPCHK(hipStreamWaitEvent(k.stream, k.ev, 0));
   }
+  k.lean_clock = ~0ull;                                    // (arbitrary actions)
   if (cog::launch_step(launch_state(k, env->host), static_cast<const uint8_t *>(d_actions), k.stream))
     return fail(COG_ERR_HIP, std::string("step launch failed: ") + hipGetErrorString(hipGetLastError()));
   return finish(env, true);
@@ -815,6 +831,7 @@ int cog_env_step(cog_env *env, const cog_action_t *actions, size_t n) {
     }
     uint32_t seq = 0, *ctr = nullptr;
     k.pub_done = false;
+    k.lean_clock = ~0ull;                                  // (arbitrary actions)
     if (env->host && k.zc && k.mir_valid && k.host_synced && cog::step_pub_ok(k.n) &&
         (ctr = signal_arm(k.done, seq))) {                 // the step publishes and signals itself
       cog::DevState ps = launch_state(k, true);
@@ -1057,7 +1074,10 @@ int cog_env_set_autoreset(cog_env *env, int on) {
   if (!env) return fail(COG_ERR_INVALID, "env is NULL");
   int rc = sync_all(env);
   if (rc) return rc;
-  for (EnvShard &k : env->sh) k.s.autoreset = on ? 1u : 0u;
+  for (EnvShard &k : env->sh) {
+    k.s.autoreset = on ? 1u : 0u;
+    k.lean_clock = ~0ull;
+  }
   return COG_OK;
 }
 
@@ -1286,6 +1306,7 @@ static int runner_launch_fused(cog_runner *r, int steps) {
     // one host-visible step with the views in sync (runner.sample(); runner.step()): the step
     // publishes itself, the sampled actions included (k_env_step_pub), as env.step() does
     if (host && steps == 1 && !r->timing && k.zc && k.mir_valid && k.host_synced && cog::step_pub_ok(k.n) && q.n) {
+      k.lean_clock = ~0ull;                                // (a full step: not the trio)
       uint8_t *h_act = const_cast<uint8_t *>(zc_device(r->smp->h_actions + q.first, q.n * COG_ACTION_BYTES));
       uint32_t seq = 0, *ctr = nullptr;
       if (h_act && zc_same_on(k.device, r->smp->h_actions + q.first) && (ctr = signal_arm(k.done, seq))) {
@@ -1307,11 +1328,19 @@ static int runner_launch_fused(cog_runner *r, int steps) {
     }
     const cog::DevState s = launch_state(k, host);
     if (r->chunk > 1) {                                    // persistent kernels, chunk steps each
-      for (int t = 0; t < steps; t += r->chunk)
-        if (cog::launch_rollout(s, src, std::min(r->chunk, steps - t), q.d_rng, q.d_actions, k.stream,
-                                r->env->n_players >= 3, &k.park_seq))
+      const bool trio = cog::rollout_kind_of(k.n, src, r->env->n_players >= 3) == 3;
+      for (int t = 0; t < steps; t += r->chunk) {
+        const int kk = std::min(r->chunk, steps - t);
+        // no env can park in this launch (EnvShard::lean_clock): no fix-up launch
+        const bool no_fixup = trio && k.s.autoreset && k.lean_clock != ~0ull &&
+                              k.lean_clock + (uint64_t)kk < (uint64_t)r->env->max_steps;
+        if (cog::launch_rollout(s, src, kk, q.d_rng, q.d_actions, k.stream, r->env->n_players >= 3, &k.park_seq,
+                                no_fixup))
           return fail(COG_ERR_HIP, std::string("rollout launch failed: ") + hipGetErrorString(hipGetLastError()));
+        k.lean_clock = trio && k.lean_clock != ~0ull ? k.lean_clock + (uint64_t)kk : ~0ull;
+      }
     } else {
+      k.lean_clock = ~0ull;                                // (full steps)
       for (int t = 0; t < steps; t++)
         if (cog::launch_sample_step(s, src, q.d_rng, q.d_actions, k.stream))
           return fail(COG_ERR_HIP, std::string("sample_step launch failed: ") + hipGetErrorString(hipGetLastError()));
@@ -1346,6 +1375,7 @@ int cog_runner_step(cog_runner *r) {
   for (size_t j = 0; j < r->env->sh.size(); j++) {
     EnvShard &k = r->env->sh[j];
     DeviceGuard g(k.device);
+    k.lean_clock = ~0ull;                                  // (a full step)
     if (cog::launch_step(launch_state(k, host), r->smp->sh[j].d_actions, k.stream))
       return fail(COG_ERR_HIP, std::string("step launch failed: ") + hipGetErrorString(hipGetLastError()));
   }

@@ -44,6 +44,7 @@ constexpr uint32_t F_SCAN_OVER = 0x40u;
 constexpr uint32_t F_B_START_LT4 = 0x80u;
 constexpr uint32_t F_BAD_ACTION = 0x100u;
 constexpr uint32_t F_SYNC_TIMEOUT = 0x200u;  // (device status only) a trio wave's progress wait timed out
+constexpr uint32_t F_PARK_NOFIX = 0x400u;    // (device status only) an env parked in a launch without a fix-up
 constexpr uint32_t F_ERROR_MASK = F_MAPGEN_FAIL | F_GRID_OVER;
 
 struct PlayerPriv {                  // Player + Deck private members (player.h:60-75, cards.h:137-145)
@@ -112,6 +113,7 @@ struct DevState {
   // the list of workgroup indices with a parked env (park_list_bytes(n))
   uint32_t *parkq;
   uint32_t park_par;
+  uint32_t no_fixup;                 // 1: no k_env_fixup follows this launch (a park is an error)
   // direct publish (launch_step_pub only; null otherwise): device addresses of the shard's pinned
   // ObsData view and outs block, and the publish mirror (k_publish's `mir`)
   uint8_t *pub_obs, *pub_outs, *pub_mir;
@@ -168,8 +170,10 @@ int launch_sample_step(const DevState &s, int mask_source, uint32_t *d_rng, uint
 // rollout's deferred turn end then runs the selected-mask loop at every shard size)
 // park_seq: the shard's count of launches with a fix-up (counts them; alternate launches use
 // alternate counters of DevState::parkq)
+// no_fixup: the caller has shown that no env can park in this launch (cog_abi.cpp EnvShard::
+// lean_clock): the trio launches alone, and a park it meets all the same is an error (F_PARK_NOFIX)
 int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions,
-                   void *stream, bool defer_ok, uint32_t *park_seq);
+                   void *stream, bool defer_ok, uint32_t *park_seq, bool no_fixup = false);
 inline size_t park_list_bytes(size_t n) { return (2 + (n + 31) / 32) * sizeof(uint32_t); }
 int rollout_kind_of(size_t n, int mask_source, bool defer_ok);   // 0 duo, 1 wave, 2 pipe, 3 trio
 int trio_epw(size_t n);                                          // envs per trio workgroup (32 or 64)

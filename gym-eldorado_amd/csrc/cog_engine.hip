@@ -2766,6 +2766,11 @@ DEV DevState wave_view(const DevState &s, size_t base) {
 // atomic per such wave), so that k_env_fixup visits only those (DevState::parkq)
 DEV void park_list_push(const DevState &s_glob, bool parked) {
   if (__builtin_amdgcn_ballot_w64(parked) && (threadIdx.x & 63) == 0) {
+    if (s_glob.no_fixup) {                                 // the host showed no park could happen
+      atomicOr(&s_glob.status[0], F_PARK_NOFIX);
+      atomicAdd(&s_glob.status[1], 1u);
+      *s_glob.err = 1u;
+    }
     const uint32_t j = atomicAdd(&s_glob.parkq[s_glob.park_par], 1u);
     s_glob.parkq[2 + j] = blockIdx.x;
   }
@@ -3511,7 +3516,7 @@ __global__ void __launch_bounds__(128) k_env_rollout_duo(DevState s, int steps, 
 // counters go to LDS only at a turn end (the drawing wave's) and at a park or the end (the epilogue's).
 constexpr int kTrioRingG = 3;
 #ifndef COG_TRIO_DEPTH                                     // (diagnostic builds: tools/r04/gpu_depth.sh)
-#define COG_TRIO_DEPTH 8
+#define COG_TRIO_DEPTH 8                                   // (16 measured the same: profiles/r05i_trio_depth16.txt)
 #endif
 constexpr int kTrioDepth = COG_TRIO_DEPTH;                 // ring slots (records in flight)
 constexpr int kTrioLead = 4;                               // presampled draws: steps ahead of the record
@@ -3526,8 +3531,8 @@ enum TrioCnt : int { CNT_REC = 0, CNT_DRAW, CNT_STA, CNT_STB, CNT_PRE, CNT_FIN, 
 constexpr uint32_t kTrioSpinLimit = 1u << 21;             // polls (~0.2 s)
 struct TrioLds {
   uint2 img[4][5][64];                // every player's compact DeckObs (the drawing wave's): piles of types 0-7
-  uint4 ring[kTrioDepth][kTrioRingG][64];   // record t (above), t % 8
-  uint32_t srng[kTrioDepth][64];      // the sampler state after step t, t % 8
+  uint4 ring[kTrioDepth][kTrioRingG][64];   // record t (above), slot t % kTrioDepth
+  uint32_t srng[kTrioDepth][64];      // the sampler state after step t, slot t % kTrioDepth
   uint3 pre[kTrioLead][64];           // step t's presampled draws, t % 4: state, head 0's draw | risk << 31, state after
   uint4 pl[4][64];
   uint4 heads[4][64];
@@ -3537,7 +3542,7 @@ struct TrioLds {
   uint32_t cnt[kTrioCnts];            // progress counters
   UidEntry tab[kUidTab];
 };
-static_assert(sizeof(TrioLds) <= 54613, "three trio workgroups per CU");
+static_assert(sizeof(TrioLds) <= 54613, "three trio workgroups per CU (trio_pad_lds keeps two)");
 static_assert((kTrioDepth & (kTrioDepth - 1)) == 0 && kTrioDepth >= 4, "ring slots: a power of two");
 
 // A wave keeps the counters it last read (wave-uniform, in SGPRs) and reads them again -- all six
@@ -3776,7 +3781,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
   TrioCnt6 cc;
   for (int t = 0; t < steps; t++) {
     const int sl = t & (kTrioDepth - 1);
-    if (t >= kTrioDepth) {                                 // slot t % 8 free
+    if (t >= kTrioDepth) {                                 // slot t % kTrioDepth free
       cnt_wait(D, cc, cc.sta, (uint32_t)(t - kTrioDepth + 1), s_glob);
       cnt_wait(D, cc, cc.stb, (uint32_t)(t - kTrioDepth + 1), s_glob);
     }
@@ -4583,7 +4588,7 @@ static unsigned fixup_grid(unsigned nblocks) {
   return std::max(1u, std::min(nblocks, cap));
 }
 int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions, void *stream,
-                   bool defer_ok, uint32_t *park_seq) {
+                   bool defer_ok, uint32_t *park_seq, bool no_fixup) {
   if (!s.n || steps <= 0) return 0;
   const int kind = rollout_kind(s.n, mask_source, defer_ok);
   if (kind == RK_DUO || kind == RK_TRIO) {
@@ -4596,6 +4601,9 @@ int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rn
     DevState sd = s;
     sd.redo_at = redo_at;
     sd.park_par = (*park_seq)++ & 1u;
+    // (the test hook parks every env: never without the fix-up; $COG_ALWAYS_FIXUP for A/B)
+    static const bool always_fixup = getenv("COG_ALWAYS_FIXUP") != nullptr;
+    sd.no_fixup = no_fixup && kind == RK_TRIO && redo_at < 0 && !always_fixup ? 1u : 0u;
     const int epw = kind == RK_TRIO ? trio_epw(s.n) : 64;
     const unsigned nb = blocks_for(s.n, epw);
     const dim3 g(nb), gf(fixup_grid(nb));
@@ -4608,7 +4616,8 @@ int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rn
       // profiles/r04t_trio_fused.txt)
       hipLaunchKernelGGL((k_env_rollout_trio<MASK_SELECTED>), g, dim3(256), trio_pad_lds(nb), st, sd, steps, epw, d_rng,
                          d_actions);
-      hipLaunchKernelGGL((k_env_fixup<MASK_SELECTED>), gf, dim3(64), 0, st, sd, steps, d_rng, d_actions, epw);
+      if (!sd.no_fixup)
+        hipLaunchKernelGGL((k_env_fixup<MASK_SELECTED>), gf, dim3(64), 0, st, sd, steps, d_rng, d_actions, epw);
     } else {
       hipLaunchKernelGGL((k_env_rollout_duo<MASK_SELECTED>), g, dim3(128), 0, st, sd, steps, d_rng, d_actions);
       hipLaunchKernelGGL((k_env_fixup<MASK_SELECTED>), gf, dim3(64), 0, st, sd, steps, d_rng, d_actions, epw);
