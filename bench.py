@@ -216,10 +216,27 @@ def host_loop(cg, n, difficulty, device, steps, use_runner):
             env.step(acts)
     for _ in range(20):
         one()
+    s0, h0 = smp.spec_stats()
     t0 = time.perf_counter()
     for _ in range(steps):
         one()
     wall = time.perf_counter() - t0
+    s1, h1 = smp.spec_stats()
+    split = None
+    if runner is None:                                    # the two calls timed apart (per call, mean)
+        ts = tt = 0.0
+        for _ in range(steps):
+            a = time.perf_counter()
+            smp.sample(masks)
+            b = time.perf_counter()
+            env.step(acts)
+            ts += b - a
+            tt += time.perf_counter() - b
+        split = {"sample_us": ts / steps * 1e6, "step_us": tt / steps * 1e6,
+                 "speculative_samples": (h1 - h0) / max(1, s1 - s0),
+                 "note": "sample(): the speculative sample the step before computed (a host copy) when "
+                         "speculative_samples = 1; step(): one k_env_step_pub launch (the step, its "
+                         "publish into the pinned views, the next sample) + its completion word"}
     # bytes of host-visible records refreshed per env-step: ObsData tail (1,088) + selected mask,
     # info, rewards, done, agent (338) + actions (64).  An upper bound of what crosses PCIe:
     # k_publish stores only the 16-B granules that changed since the last refresh, and the
@@ -232,7 +249,8 @@ def host_loop(cg, n, difficulty, device, steps, use_runner):
             "view_refresh_GBs_nominal": n * (d2h + h2d) * steps / wall / 1e9,
             "note": "d2h/h2d bytes are the records refreshed per env-step (upper bound): k_publish "
                     "moves only the changed 16-B granules over PCIe",
-            "loop": "runner.sample(); runner.step_sync()" if use_runner else "sampler.sample(masks); env.step(actions)"}
+            "loop": "runner.sample(); runner.step_sync()" if use_runner else "sampler.sample(masks); env.step(actions)",
+            "split": split}
 
 
 def time_reset_c2(cg, dev, calls=100):

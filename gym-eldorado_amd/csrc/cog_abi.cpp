@@ -295,6 +295,7 @@ struct cog_env {
   size_t n = 0;
   uint8_t n_players = 4;              // the batch's players (reset params; the default ctor's 4)
   uint32_t max_steps = 0;             // the last reset's max_steps (0: unknown)
+  uint64_t version = 0;               // calls that changed the env state so far (SamplerSpec)
   std::vector<EnvShard> sh;
   uint32_t *h_err = nullptr;          // pinned, device-mapped: one error word per shard (256 B apart)
   // host views: obs is one pinned allocation; the small records are the shard's h_outs block
@@ -319,11 +320,33 @@ struct SamplerShard {
   Signal done;                        // completion word (cog_sampler::h_sig)
 };
 
+// The speculative next sample (single-shard samplers and envs; cog::SampleSpec).  The reference's
+// host loop is `sampler.sample(env.selected_action_masks); env.step(sampler.get_actions())`
+// (benchmarks.py:47-51): when env.step gets a sampler's own actions view, the step kernel also
+// samples that sampler's next actions from the selected masks the step leaves -- with the
+// sampler's own state, into spare buffers -- and the sampler's next sample() of the env's own mask
+// view takes them: a host copy of the actions and a swap of the state and device-action buffers,
+// no launch.  It applies only while nothing has touched the env or the sampler since (version
+// counters), no episode ended in the step (its reset is not speculated), and the sampler's device
+// actions were never handed out (a swap would break an alias); otherwise sample() runs as always.
+struct SamplerSpec {
+  uint32_t *d_rng = nullptr;          // spare state buffer (device)
+  uint8_t *d_actions = nullptr;       // spare ActionData records (device)
+  uint8_t *h = nullptr;               // pinned, device-mapped: n x 8 B actions, then the invalid word
+  cog_env *env = nullptr;             // the env whose step speculated, at version env_version
+  uint64_t env_version = 0, version = 0;
+  bool ok = false;
+};
+
 struct cog_sampler {
   size_t n = 0;
   std::vector<SamplerShard> sh;
   cog_action_t *h_actions = nullptr;  // persistent pinned view, all shards
   uint32_t *h_sig = nullptr;          // pinned, device-mapped: one completion word per shard (256 B apart)
+  uint64_t version = 0;               // samples so far (every path)
+  uint64_t spec_hits = 0;             // of them, the speculative sample taken
+  bool exported = false;              // device actions handed out (cog_sampler_device_actions)
+  SamplerSpec spec;
 };
 
 struct cog_runner {
@@ -360,6 +383,24 @@ void host_env_register(cog_env *e, bool on) {
   if (!on && it != g_host_envs.end()) g_host_envs.erase(it);
 }
 
+std::vector<cog_sampler *> g_samplers;   // (under g_host_envs_mu)
+void sampler_register(cog_sampler *s, bool on) {
+  std::lock_guard<std::mutex> lk(g_host_envs_mu);
+  auto it = std::find(g_samplers.begin(), g_samplers.end(), s);
+  if (on && it == g_samplers.end()) g_samplers.push_back(s);
+  if (!on && it != g_samplers.end()) g_samplers.erase(it);
+}
+// the single-shard sampler whose pinned actions view `actions` is (null: none)
+cog_sampler *sampler_of_actions(const cog_action_t *actions, size_t n) {
+  std::lock_guard<std::mutex> lk(g_host_envs_mu);
+  for (cog_sampler *s : g_samplers)
+    if (s->h_actions == actions && s->n == n && s->sh.size() == 1) return s;
+  return nullptr;
+}
+bool env_alive(const cog_env *e) {
+  std::lock_guard<std::mutex> lk(g_host_envs_mu);
+  return std::find(g_host_envs.begin(), g_host_envs.end(), e) != g_host_envs.end();
+}
 EnvShard *env_masks_in_hbm(const cog_action_mask_t *masks, size_t n, int device) {
   if (std::getenv("COG_NO_HBM_MASKS")) return nullptr;    // (A/B)
   std::lock_guard<std::mutex> lk(g_host_envs_mu);
@@ -593,6 +634,13 @@ cog::DevState launch_state(const EnvShard &k, bool host_views) {
 
 void sampler_free(cog_sampler *s) {
   if (!s) return;
+  sampler_register(s, false);
+  if (!s->sh.empty()) {
+    DeviceGuard g(s->sh[0].device);
+    if (s->spec.d_rng) (void)hipFree(s->spec.d_rng);
+    if (s->spec.d_actions) (void)hipFree(s->spec.d_actions);
+  }
+  zc_free(s->spec.h);
   for (SamplerShard &k : s->sh) {
     DeviceGuard g(k.device);
     if (k.stream) (void)hipStreamSynchronize(k.stream);
@@ -745,6 +793,7 @@ int cog_env_shard_info(const cog_env *env, int k, size_t *first, size_t *count, 
 static int env_reset_impl(cog_env *e, const cog::ResetParams &p) {
   int rc = prepare_host(e);
   if (rc) return rc;
+  e->version++;
   if (p.use_params) {
     e->n_players = p.n_players;
     e->max_steps = p.max_steps;
@@ -802,6 +851,7 @@ int cog_env_step_device_stream(cog_env *env, const void *d_actions, size_t n, vo
   DeviceGuard g(k.device);
   int rc = prepare_host(env);
   if (rc) return rc;
+  env->version++;
   if (stream != COG_NO_STREAM) {      // the caller's stream produced the actions: order after it
     HIPCHK(hipEventRecord(k.ev, static_cast<hipStream_t>(stream)));   // (NULL: the null stream)
     HIPCHK(hipStreamWaitEvent(k.stream, k.ev, 0));
@@ -816,11 +866,32 @@ int cog_env_step_device(cog_env *env, const void *d_actions, size_t n) {
   return cog_env_step_device_stream(env, d_actions, n, COG_NO_STREAM);
 }
 
+// spare buffers of a single-shard sampler for the speculative sample (allocated on first use)
+static bool spec_ready(cog_sampler *q) {
+  SamplerSpec &sp = q->spec;
+  if (sp.h) return true;
+  DeviceGuard g(q->sh[0].device);
+  if (dmalloc(&sp.d_rng, q->n * sizeof(uint32_t)) || dmalloc(&sp.d_actions, q->n * COG_ACTION_BYTES) ||
+      zc_alloc(&sp.h, q->n * 8 + 64)) {
+    (void)hipGetLastError();
+    return false;
+  }
+  std::memset(sp.h, 0, q->n * 8 + 64);
+  return hipMemset(sp.d_actions, 0, q->n * COG_ACTION_BYTES) == hipSuccess;
+}
+
 int cog_env_step(cog_env *env, const cog_action_t *actions, size_t n) {
   if (!env || (!actions && n)) return fail(COG_ERR_INVALID, "NULL argument");
   if (n != env->n) return fail(COG_ERR_INVALID, "actions length != num_envs");
   int rc = prepare_host(env);
   if (rc) return rc;
+  env->version++;
+  // the actions are a sampler's own view: its next sample, speculatively (SamplerSpec)
+  cog_sampler *q = single(env) && n ? sampler_of_actions(actions, n) : nullptr;
+  if (q && (q->exported || q->sh[0].device != env->sh[0].device || std::getenv("COG_NO_SPEC") || !spec_ready(q)))
+    q = nullptr;
+  if (q) q->spec.ok = false;
+  bool spec_launched = false;
   for (EnvShard &k : env->sh) {
     if (!k.n) continue;
     DeviceGuard g(k.device);
@@ -838,7 +909,16 @@ int cog_env_step(cog_env *env, const cog_action_t *actions, size_t n) {
       ps.pub_obs = k.h_obs_d;
       ps.pub_outs = k.h_outs_d;
       ps.pub_mir = k.mir;
-      if (cog::launch_step_pub(ps, da, k.stream, ctr, k.done.d, seq))
+      cog::SampleSpec sp{nullptr, nullptr, nullptr, nullptr, nullptr};
+      if (q) {
+        uint8_t *h = const_cast<uint8_t *>(zc_device(q->spec.h, n * 8 + 64));
+        if (h) {
+          *reinterpret_cast<volatile uint32_t *>(q->spec.h + n * 8) = 0u;   // the invalid word
+          sp = cog::SampleSpec{q->sh[0].d_rng, q->spec.d_rng, q->spec.d_actions, h, reinterpret_cast<uint32_t *>(h + n * 8)};
+          spec_launched = true;
+        }
+      }
+      if (cog::launch_step_pub(ps, da, k.stream, ctr, k.done.d, seq, spec_launched ? &sp : nullptr))
         return fail(COG_ERR_HIP, std::string("step launch failed: ") + hipGetErrorString(hipGetLastError()));
       signal_armed(k.done);
       k.pub_done = true;
@@ -847,7 +927,14 @@ int cog_env_step(cog_env *env, const cog_action_t *actions, size_t n) {
     if (cog::launch_step(launch_state(k, env->host), da, k.stream))
       return fail(COG_ERR_HIP, std::string("step launch failed: ") + hipGetErrorString(hipGetLastError()));
   }
-  return finish(env, true);
+  rc = finish(env, true);
+  if (!rc && spec_launched) {                              // the step has completed: its speculation stands
+    q->spec.env = env;
+    q->spec.env_version = env->version;
+    q->spec.version = q->version;
+    q->spec.ok = true;
+  }
+  return rc;
 }
 
 static int alloc_host_views(cog_env *env) {
@@ -1074,6 +1161,7 @@ int cog_env_set_autoreset(cog_env *env, int on) {
   if (!env) return fail(COG_ERR_INVALID, "env is NULL");
   int rc = sync_all(env);
   if (rc) return rc;
+  env->version++;
   for (EnvShard &k : env->sh) {
     k.s.autoreset = on ? 1u : 0u;
     k.lean_clock = ~0ull;
@@ -1136,6 +1224,7 @@ int cog_sampler_create_multi(size_t n_envs, uint64_t seed, const int *devices, i
       return fail(COG_ERR_HIP, "sampler init failed");
     }
   }
+  sampler_register(s, true);
   *out = s;
   return COG_OK;
 }
@@ -1171,6 +1260,7 @@ static int sampler_run(SamplerShard &k, cog_action_t *h_actions, const uint8_t *
 int cog_sampler_sample_device(cog_sampler *s, const void *d_masks, size_t n) {
   if (!s || !d_masks) return fail(COG_ERR_INVALID, "NULL argument");
   if (n != s->n) return fail(COG_ERR_INVALID, "action_mask length != num_envs");
+  s->version++;
   if (s->sh.size() != 1) return fail(COG_ERR_INVALID, "device masks need a single-shard sampler (one device pointer)");
   SamplerShard &k = s->sh[0];
   DeviceGuard g(k.device);
@@ -1183,6 +1273,22 @@ int cog_sampler_sample_device(cog_sampler *s, const void *d_masks, size_t n) {
 int cog_sampler_sample(cog_sampler *s, const cog_action_mask_t *masks, size_t n) {
   if (!s || (!masks && n)) return fail(COG_ERR_INVALID, "NULL argument");
   if (n != s->n) return fail(COG_ERR_INVALID, "action_mask length != num_envs");
+  SamplerSpec &sp = s->spec;
+  const bool hit = sp.ok && sp.version == s->version && sp.env && env_alive(sp.env) && single(sp.env) &&
+                   masks == sp.env->h_sel && sp.env->n == n && sp.env->version == sp.env_version &&
+                   *reinterpret_cast<volatile uint32_t *>(sp.h + n * 8) == 0u;
+  sp.ok = false;
+  s->version++;
+  if (hit) {                                               // the env's step sampled these masks already
+    SamplerShard &k = s->sh[0];
+    std::swap(k.d_rng, sp.d_rng);
+    std::swap(k.d_actions, sp.d_actions);
+    const uint64_t *src = reinterpret_cast<const uint64_t *>(sp.h);
+    uint8_t *dst = reinterpret_cast<uint8_t *>(s->h_actions);
+    for (size_t i = 0; i < n; i++) *reinterpret_cast<uint64_t *>(dst + i * COG_ACTION_BYTES) = src[i];
+    s->spec_hits++;
+    return COG_OK;
+  }
   for (SamplerShard &k : s->sh) k.done.queued = false;
   for (SamplerShard &k : s->sh) {
     if (!k.n) continue;
@@ -1214,12 +1320,23 @@ int cog_sampler_sample(cog_sampler *s, const cog_action_mask_t *masks, size_t n)
 }
 
 cog_action_t *cog_sampler_actions(cog_sampler *s) { return s ? s->h_actions : nullptr; }
-void *cog_sampler_device_actions(cog_sampler *s) { return s ? (void *)s->sh[0].d_actions : nullptr; }
+void *cog_sampler_device_actions(cog_sampler *s) {
+  if (!s) return nullptr;
+  s->exported = true;                                      // (aliases: no buffer swaps from now on)
+  return (void *)s->sh[0].d_actions;
+}
 void *cog_sampler_shard_device_actions(cog_sampler *s, int k) {
   if (!s || k < 0 || (size_t)k >= s->sh.size()) return nullptr;
+  s->exported = true;
   return (void *)s->sh[k].d_actions;
 }
 int cog_sampler_device(const cog_sampler *s) { return s ? s->sh[0].device : -1; }
+int cog_sampler_spec_stats(const cog_sampler *s, uint64_t *samples, uint64_t *hits) {
+  if (!s || !samples || !hits) return fail(COG_ERR_INVALID, "NULL argument");
+  *samples = s->version;
+  *hits = s->spec_hits;
+  return COG_OK;
+}
 
 // ---- runner ------------------------------------------------------------------------------
 int cog_runner_create(cog_env *env, cog_sampler *s, size_t n_threads, uint32_t flags, cog_runner **out) {
@@ -1258,6 +1375,7 @@ static bool runner_host(const cog_runner *r) { return !(r->flags & COG_RUNNER_DE
 static int runner_flush_sample(cog_runner *r) {
   if (!r->pending_sample) return COG_OK;
   r->pending_sample = false;
+  r->smp->version++;
   // a lone sample reads the selected masks, as the reference runner's does (runner.h:26,48);
   // stored-mask sampling exists only fused with a step
   for (size_t j = 0; j < r->env->sh.size(); j++) {
@@ -1296,6 +1414,8 @@ static void views_pending(EnvShard &k) {
 
 static int runner_launch_fused(cog_runner *r, int steps) {
   const int src = (r->flags & COG_RUNNER_STORED_MASKS) ? cog::MASK_STORED : cog::MASK_SELECTED;
+  r->env->version++;
+  r->smp->version++;
   const bool host = runner_host(r);
   int rc;
   if (host && (rc = prepare_host(r->env))) return rc;
@@ -1364,6 +1484,7 @@ int cog_runner_sample(cog_runner *r) {
 
 int cog_runner_step(cog_runner *r) {
   if (!r) return fail(COG_ERR_INVALID, "runner is NULL");
+  r->env->version++;
   if (r->pending_sample) {
     r->pending_sample = false;
     return runner_launch_fused(r, 1);

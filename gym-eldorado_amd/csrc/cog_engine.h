@@ -143,8 +143,19 @@ int launch_step(const DevState &s, const uint8_t *d_actions, void *stream);
 // comparison, and the last workgroup copies the status granules and stores the completion word
 // (sig_ctr: a zeroed device counter).  Returns -1 when the batch is too large for it
 // (step_pub_ok).
+// The speculative next sample of a host step (launch_step_pub): env.step(actions) whose actions
+// are a sampler's view samples that sampler's next actions from the step's new selected masks into
+// spare buffers, so that the sampler's next sample of the env's own masks is a host copy
+// (cog_abi.cpp SamplerSpec).  rng_in null: none.
+struct SampleSpec {
+  const uint32_t *rng_in;            // the sampler's state
+  uint32_t *rng_out;                 // its state after the speculative sample
+  uint8_t *act_dev;                  // ActionData records (device)
+  uint8_t *act_host;                 // 8 B per env: device address of pinned staging
+  uint32_t *invalid;                 // device address of a pinned word: 1 when an env's episode ended
+};
 int launch_step_pub(const DevState &s, const uint8_t *d_actions, void *stream, uint32_t *sig_ctr, uint32_t *sig_word,
-                    uint32_t seq);
+                    uint32_t seq, const SampleSpec *spec = nullptr);
 bool step_pub_ok(size_t n);
 // the runner's fused sample + step in the same form; the sampled actions also go to the sampler's
 // pinned view (h_actions, device address)

@@ -2597,7 +2597,7 @@ DEV void pub_env_compare(const DevState &s, size_t i) {
 template <int SRC>
 __global__ void __launch_bounds__(64) k_env_step_pub(DevState s, const uint8_t *__restrict__ act_in, uint32_t *__restrict__ rngs,
                                                      uint8_t *__restrict__ actions_out, uint8_t *__restrict__ h_actions,
-                                                     GridSignal sig) {
+                                                     GridSignal sig, SampleSpec spec) {
   __shared__ UidEntry tab[kUidTab];
   uid_tab_fill(tab);
   const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2613,6 +2613,18 @@ __global__ void __launch_bounds__(64) k_env_step_pub(DevState s, const uint8_t *
     __builtin_amdgcn_s_waitcnt(0);                         // stored, including other lanes' encode
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     if (ended) pub_env_compare(s, i);
+  }
+  if (SRC == MASK_EXTERNAL && spec.rng_in && i0 < s.n) {   // the sampler's next sample, speculative:
+    if (ended) {                                           // from the selected mask this step left (an
+      *spec.invalid = 1u;                                  // ended episode's reset: no speculation)
+    } else {
+      uint32_t rng = spec.rng_in[i];
+      uint8_t a[5];
+      sample_heads(heads_of(mbits_of(s.heads[5 * i])), rng, a, tab);   // (this lane's own store)
+      spec.rng_out[i] = rng;
+      store_action(spec.act_dev + i * COG_ACTION_BYTES, a);
+      store_action(spec.act_host + i * 8, a);
+    }
   }
   // completion: the last workgroup to arrive publishes the status granules, then the word
   __syncthreads();
@@ -4472,22 +4484,24 @@ int launch_step(const DevState &s, const uint8_t *d_actions, void *stream) {
 constexpr unsigned kStepPubMaxBlocks = 128;              // (completion counter arrivals)
 bool step_pub_ok(size_t n) { return n && blocks_for(n, 64) <= kStepPubMaxBlocks; }
 int launch_step_pub(const DevState &s, const uint8_t *d_actions, void *stream, uint32_t *sig_ctr, uint32_t *sig_word,
-                    uint32_t seq) {
+                    uint32_t seq, const SampleSpec *spec) {
   if (!step_pub_ok(s.n) || !sig_ctr || !s.pub_obs || !s.pub_outs || !s.pub_mir) return -1;
+  const SampleSpec none{nullptr, nullptr, nullptr, nullptr, nullptr};
   hipLaunchKernelGGL(k_env_step_pub<MASK_EXTERNAL>, dim3(blocks_for(s.n, 64)), dim3(64), 0, (hipStream_t)stream, s,
-                     d_actions, nullptr, nullptr, nullptr, GridSignal{sig_ctr, sig_word, seq});
+                     d_actions, nullptr, nullptr, nullptr, GridSignal{sig_ctr, sig_word, seq}, spec ? *spec : none);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_sample_step_pub(const DevState &s, int mask_source, uint32_t *d_rng, uint8_t *d_actions, uint8_t *h_actions,
                            void *stream, uint32_t *sig_ctr, uint32_t *sig_word, uint32_t seq) {
   if (!step_pub_ok(s.n) || !sig_ctr || !s.pub_obs || !s.pub_outs || !s.pub_mir || !h_actions) return -1;
   const dim3 g(blocks_for(s.n, 64)), b(64);
+  const SampleSpec none{nullptr, nullptr, nullptr, nullptr, nullptr};
   if (mask_source == MASK_STORED)
     hipLaunchKernelGGL(k_env_step_pub<MASK_STORED>, g, b, 0, (hipStream_t)stream, s, nullptr, d_rng, d_actions, h_actions,
-                       GridSignal{sig_ctr, sig_word, seq});
+                       GridSignal{sig_ctr, sig_word, seq}, none);
   else
     hipLaunchKernelGGL(k_env_step_pub<MASK_SELECTED>, g, b, 0, (hipStream_t)stream, s, nullptr, d_rng, d_actions,
-                       h_actions, GridSignal{sig_ctr, sig_word, seq});
+                       h_actions, GridSignal{sig_ctr, sig_word, seq}, none);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_sample(size_t n, const uint8_t *d_masks, uint32_t *d_rng, uint8_t *d_actions, void *stream,

@@ -475,6 +475,11 @@ PYBIND11_MODULE(_city_of_gold, m) {
         return view(s.actions(), s.num_envs(), self, true);   // an input of env.step: writable
       })
       .def("sample", &VecSampler::sample, "action_mask"_a)
+      .def("spec_stats", [](VecSampler &s) {
+        uint64_t samples = 0, hits = 0;
+        check(cog_sampler_spec_stats(s.handle(), &samples, &hits));
+        return py::make_tuple(samples, hits);
+      }, "(samples, speculative samples taken): cog_sampler_spec_stats")
       .def("device_actions", [](VecSampler &s, int k) {
         return (uintptr_t)cog_sampler_shard_device_actions(s.handle(), k);
       }, "shard"_a = 0)

@@ -185,6 +185,10 @@ COG_API cog_action_t *cog_sampler_actions(cog_sampler *s);   /* persistent host 
 COG_API void *cog_sampler_device_actions(cog_sampler *s);    /* device view (shard 0) */
 COG_API void *cog_sampler_shard_device_actions(cog_sampler *s, int shard);
 COG_API int cog_sampler_device(const cog_sampler *s);       /* device ordinal */
+/* samples so far, and how many of them took the speculative sample of the env step before them
+ * (env.step(actions) with this sampler's actions view samples the next actions from the masks it
+ * leaves; sample() of that env's own mask view then needs no launch).  Diagnostics. */
+COG_API int cog_sampler_spec_stats(const cog_sampler *s, uint64_t *samples, uint64_t *hits);
 
 /* ---- runner: asynchronous sample/step on the env's streams (runner.h:81-100) ---------------- */
 COG_API int cog_runner_create(cog_env *env, cog_sampler *s, size_t n_threads, uint32_t flags,

@@ -98,3 +98,44 @@ def test_sampler_on_env_view_orders_after_async_step(cg):
         assert po.named_equal(smp2.get_actions(), osm2.actions) is None, f"step {t}: sampled before the step"
         bad = po.named_equal(env.selected_action_masks, orc.selected_action_masks)
         assert bad is None, f"step {t}: {bad}"
+
+
+def test_speculative_sample_exact(cg):
+    """The reference host loop `sampler.sample(env.selected_action_masks); env.step(actions)`
+    (benchmarks.py:47-51) takes the sample the step computed speculatively (cog_abi.cpp
+    SamplerSpec): actions, sampler state and views stay bit-exact with the oracle through hits and
+    through everything that must void the speculation -- another sampler stepping the env, a
+    sample of other masks, a reset, an episode end, a runner step."""
+    n, seed = 256, 4711
+    env, smp, orc, osm = make(cg, n, seed, max_steps=25)
+    other = cg.vec.get_vec_sampler(n)(999)
+    oother = po.OracleSampler(n, 999)
+    masks, acts = env.selected_action_masks, smp.get_actions()
+
+    def check(t, what):
+        for nm in ("observations", "selected_action_masks", "infos"):
+            bad = po.named_equal(getattr(env, nm), getattr(orc, nm))
+            assert bad is None, f"{what} step {t}: {nm}.{bad}"
+        assert np.array_equal(env.dones, orc.dones) and np.array_equal(env.agent_selection, orc.agent_selection)
+
+    ended = 0
+    for t in range(400):
+        if t == 150:                                         # another sampler steps the env once
+            other.sample(masks)
+            oother.sample(orc.selected_action_masks)
+            env.step(other.get_actions())
+            orc.step(oother.actions)
+        if t == 300:                                         # a reset voids the speculation
+            env.reset(seed + 1, 4, 3, cg.HARD, 25, False)
+            orc.reset(seed + 1, 4, 3, 2, 25)
+        if t % 97 == 5:                                      # a sample of a copy of the masks
+            smp.sample(masks.copy())
+        else:
+            smp.sample(masks)
+        osm.sample(orc.selected_action_masks)
+        assert po.named_equal(acts, osm.actions) is None, f"sample at step {t}"
+        env.step(acts)
+        orc.step(osm.actions)
+        check(t, "host loop")
+        ended += int(orc.dones.sum())
+    assert ended > 0, "no episode ended: the test lost a case"
