@@ -3611,7 +3611,20 @@ DEV void cnt_wait(TrioLds &D, TrioCnt6 &c, const uint32_t &field, uint32_t v, co
     __builtin_amdgcn_s_sleep(2);
   }
 }
-DEV uint3 pre_pack(const uint4 p) { return make_uint3(p.x, p.y | p.w << 31, p.z); }
+// the stepping wave's presampled record: {the state the step starts from, head 0's index for every
+// play-head size k = 2..9 (4 bits each: uid_tab_accepted of the first draw, the narrow hand's play
+// head holds at most the pass bit and types 0-7), the state after the five draws | any draw could be
+// rejected << 31} -- the divisions off the stepping wave's chain (storing wave B has the slack)
+DEV uint3 pre_pack(const uint4 p, bool jtab) {
+  if (!jtab) return make_uint3(p.x, p.y, p.z | p.w << 31);   // head 0's draw itself
+  uint32_t jt = 0u;
+#pragma unroll
+  for (int k = 2; k <= 9; k++) {
+    const UidEntry e = uid_entry((uint32_t)k);
+    jt |= uid_tab_accepted(p.y, e.s, e.m) << (4 * (k - 2));
+  }
+  return make_uint3(p.x, jt, p.z | p.w << 31);
+}
 
 // the epilogue's player records (lds_store_wave without the neighbourhood caches)
 DEV void trio_store_players(const TrioLds &D, const DevState &s, int ne) {
@@ -3698,11 +3711,16 @@ DEV uint32_t nth_set_bit_iter(uint32_t m, uint32_t j) {
 // head 0's draw from the presampled record when the state is the one it starts from and heads
 // 1-4 are {0} (then the five draws are the presampled ones: act 1-4 = 0); false: sample the
 // sequential way
-DEV bool sample_lean(const MBits &sel, const uint3 &pr, uint32_t &rng, uint32_t &a0, const UidEntry *tab) {
+DEV bool sample_lean(const MBits &sel, const uint3 &pr, uint32_t &rng, uint32_t &a0, bool jtab, const UidEntry *tab) {
   const uint32_t m0 = sel.w0 & 0x3fffffu, k0 = __popc(m0);
-  if (!(pr.x == rng && (pr.y >> 31) == 0u && heads14_zero(sel) && k0 >= 1u)) return false;
-  const UidEntry e0 = tab[k0];
-  const uint32_t j = k0 >= 2u ? uid_tab_accepted(pr.y & 0x7fffffffu, e0.s, e0.m) : 0u;
+  if (!(pr.x == rng && (pr.z >> 31) == 0u && heads14_zero(sel) && k0 >= 1u && k0 <= 9u)) return false;
+  uint32_t j;
+  if (jtab) {
+    j = k0 >= 2u ? (pr.y >> (4u * (k0 - 2u))) & 15u : 0u;
+  } else {
+    const UidEntry e0 = tab[k0];
+    j = k0 >= 2u ? uid_tab_accepted(pr.y, e0.s, e0.m) : 0u;
+  }
   a0 = nth_set_bit_iter(m0, j);
   rng = pr.z;
   return true;
@@ -3722,8 +3740,7 @@ DEV void trio_store_private(const DevState &s, size_t i, const RegEnv &R, const 
   uint4 *pw = reinterpret_cast<uint4 *>(s.priv + i);
   reinterpret_cast<uint3 *>(reinterpret_cast<uint32_t *>(pw) + 1)[0] = make_uint3(R.seed, R.max_steps, R.turn_counter);
   pw[1] = make_uint4(R.g1x, R.g1y, R.in_market, R.flags);
-  reinterpret_cast<uint32_t *>(pw + 3)[0] = R.info_steps;
-  s.heads[5 * i] = mbits_u4(selb);
+  s.heads[5 * i] = mbits_u4(selb);                         // (Info steps: storing wave A's)
 }
 
 template <int SRC>
@@ -3805,7 +3822,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     if (live) {
       const uint32_t srng0 = srng;
       const uint3 pr = D.pre[t & (kTrioLead - 1)][l];
-      const bool fast = sample_lean(selb, pr, srng, a_play, R.tab);
+      const bool fast = sample_lean(selb, pr, srng, a_play, s_glob.trio_jt != 0u, R.tab);
       bool other = false;                                  // an action head other than play set
       if (__builtin_amdgcn_ballot_w64(!fast) && !fast) {   // (wave-uniform skip)
         uint8_t act[5];
@@ -3826,21 +3843,12 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
         park = (uint32_t)t | kParkRedo;
         live = false;
       } else if (!was_done) {                              // cog_env::step, the lean case
-        stepped = true;
-        const uint32_t info = ((R.info_steps >> (8 * ag)) + 1u) & 0xffu;   // Info steps_taken (u8)
-        R.info_steps = (R.info_steps & ~(0xffu << (8 * ag))) | (info << (8 * ag));
-        uint32_t phase = R.sh[0] & 0xffu;
+        stepped = true;                                    // (Info steps and the resources: storing
+        uint32_t phase = R.sh[0] & 0xffu;                  // wave A's)
         if (phase == COG_PHASE_INACTIVE) phase = COG_PHASE_MOVEMENT;
         steps_taken = (steps_taken + 1u) & 0xffu;
-        float r0 = __uint_as_float(R.sh[1]), r1 = __uint_as_float(R.sh[2]), r2 = __uint_as_float(R.sh[3]);
         if (a_play) {                                      // Player::play_card (player.cpp:45-60)
           const int c = (int)a_play - 1;
-          if (phase == COG_PHASE_MOVEMENT) {
-            r0 = (float)cardf(kRes0, c); r1 = (float)cardf(kRes1, c); r2 = (float)cardf(kRes2, c);
-          } else if (phase == COG_PHASE_BUYING) {
-            const uint32_t coin = cardf(kRes2, c);
-            r2 = r2 + (coin > 0 ? (float)coin : 0.5f);
-          }
           const uint32_t prev = hand_take(H, c);           // Deck::activate's hand part (the active
           n_in_hand = (n_in_hand - 1u) & 0xffu;            // pile: the drawing wave, trio_drawer)
           const bool pl = prev > 1u;
@@ -3862,11 +3870,9 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
           R.set_agent((uint32_t)na);
           selb = stnb;                                     // load_actionmask (na != ag: >= 3 players)
           stnb.w2 = (stnb.w2 & ~kMoveShopBits) | 0x204u;   // update_observation, INACTIVE phase
-          r0 = r1 = r2 = 0.f;
           R.turn_counter++;
         }
         R.sh[0] = (R.sh[0] & ~0xffu) | phase;
-        R.sh[1] = __float_as_uint(r0); R.sh[2] = __float_as_uint(r1); R.sh[3] = __float_as_uint(r2);
         // done (environment.cpp:183-207): the (next) agent's cell or the turn counter
         const uint2 cc = turn_end ? cells_n : cells_a;
         const uint32_t c0 = R.use_cell(cc, 0);
@@ -3911,10 +3917,9 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     if (live) {
       // the acting player's counters: the drawing wave's at its turn end, the epilogue's at a park
       if (tc || ended) D.pl[ag][l] = pack_lean_player(pp, n_in_hand, n_active, steps_taken);
-      const uint32_t info = (R.info_steps >> (8 * ag)) & 0xffu;
-      const uint32_t meta = kMetaValid | (uint32_t)ag << 2 | (uint32_t)na << 4 | (uint32_t)na1 << 6 | info << 8 |
+      const uint32_t meta = kMetaValid | (uint32_t)ag << 2 | (uint32_t)na << 4 | (uint32_t)na1 << 6 |
                             (ended ? kMetaEnded : 0u) | (stepped ? kMetaStepped : 0u) | (uint32_t)ag1 << 24;
-      ring[0][l] = make_uint4(R.sh[0], R.sh[1], R.sh[2], R.sh[3]);
+      ring[0][l].x = R.sh[0];                              // (the resources: storing wave A's)
       ring[1][l] = make_uint4(selb.w0, selb.w1, selb.w2, meta);
       ring[2][l] = make_uint4(stab.w0, stab.w1, stab.w2, a_play | (n_active & 0xffu) << 8);
       D.srng[sl][l] = srng;
@@ -4087,10 +4092,14 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
   E.flags = 0u;
   E.avail = 0u;
   uint32_t x = 1u;                                         // B: the sampler state at step 0
+  uint32_t infob = 0u, ph = 0u;                            // A: Info steps (u8 per player), the phase
+  float q0 = 0.f, q1 = 0.f, q2 = 0.f;                      // A: and the resources before the record
   if (live) {
     if (PART == 0) {
       const uint4 *sh4 = reinterpret_cast<const uint4 *>(s.obs + i * COG_OBS_BYTES + COG_OBS_PHASE);
       shb0 = sh4[0];
+      ph = shb0.x & 0xffu;
+      q0 = __uint_as_float(shb0.y); q1 = __uint_as_float(shb0.z); q2 = __uint_as_float(shb0.w);
       const uint4 sh1 = sh4[1], sh2 = sh4[2];
       const uint4 *pv4 = reinterpret_cast<const uint4 *>(s.priv + i);
 #pragma unroll
@@ -4099,6 +4108,7 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
         cells[p] = reinterpret_cast<const uint2 *>(pv4 + 8)[p];
       }
       const uint4 g1 = pv4[1];
+      infob = reinterpret_cast<const uint32_t *>(pv4 + 3)[0];   // EnvPriv granule 3, dword 0
       const uint32_t w[5] = {sh1.x, sh1.y, sh1.z, sh1.w, sh2.x};
       E.avail = shop_avail_of(w, (g1.y >> 8) & 0xffu, g1.z);   // (no purchase in the lean step: fixed)
     } else {
@@ -4110,7 +4120,7 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
 #pragma unroll
     for (int k = 0; k < kTrioLead; k++) {
       const uint4 p = presample(x);
-      D.pre[k][l] = pre_pack(p);
+      D.pre[k][l] = pre_pack(p, s_glob.trio_jt != 0u);
       x = p.z;
     }
   }
@@ -4130,16 +4140,15 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
       const uint4 m = D.ring[sl][1][l];
       const uint32_t meta = m.w;
       const bool rec = live && (meta & kMetaValid);
-      const int ag = (int)((meta >> 2) & 3u);
       if (rec && r + kTrioLead < steps)                    // step r + 4's draws: the state after step r,
-        D.pre[(r + kTrioLead) & (kTrioLead - 1)][l] = pre_pack(presample(mr_jump(D.srng[sl][l], kPow15)));
+        D.pre[(r + kTrioLead) & (kTrioLead - 1)][l] = pre_pack(presample(mr_jump(D.srng[sl][l], kPow15)), s_glob.trio_jt != 0u);
       cnt_store(D, CNT_PRE, (uint32_t)(r + 1));            // + 15 draws (steps r + 1 .. r + 3)
+      const uint32_t a_play = D.ring[sl][2][l].w & 0xffu;
       if (rec) {
-        s.info[i * COG_INFO_BYTES + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag] = (uint8_t)(meta >> 8);
         const MBits bs{m.x, m.y, m.z};
         store_mask_record(reinterpret_cast<uint4 *>(s.sel + i * COG_MASK_BYTES), bs, mask_diff_granules(bs, selb));
         selb = bs;
-        reinterpret_cast<uint2 *>(av + i * COG_ACTION_BYTES)[0] = make_uint2(D.ring[sl][2][l].w & 0xffu, 0u);   // (lean: heads 1-4 are 0)
+        reinterpret_cast<uint2 *>(av + i * COG_ACTION_BYTES)[0] = make_uint2(a_play, 0u);   // (lean: heads 1-4 are 0)
         if (!(meta & kMetaEnded)) {                        // dones[i] = 0, agent_selection[i]
           const uint32_t agent = meta >> 24;               // (an ended episode: k_env_fixup)
           if (out & 0xffu) s.done[i] = 0;
@@ -4158,7 +4167,26 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
     const bool rec = live && (meta & kMetaValid);
     const int ag = (int)((meta >> 2) & 3u), na = (int)((meta >> 4) & 3u);
     if (rec && PART == 0) {
-      const uint4 g0 = D.ring[sl][0][l], xa = D.ring[sl][2][l], oa = D.stbA[ag][l];
+      const uint4 xa = D.ring[sl][2][l], oa = D.stbA[ag][l];
+      const uint32_t px = D.ring[sl][0][l].x;
+      if (meta & kMetaStepped) {                           // Info steps_taken (u8) and the step's
+        infob = (infob & ~(0xffu << (8 * ag))) | ((((infob >> (8 * ag)) + 1u) & 0xffu) << (8 * ag));
+        const uint32_t phase = ph == COG_PHASE_INACTIVE ? (uint32_t)COG_PHASE_MOVEMENT : ph;
+        const uint32_t a_play = xa.w & 0xffu;              // resources (the stepping wave leaves them)
+        if (a_play) {                                      // Player::play_card (player.cpp:45-60)
+          const int c = (int)a_play - 1;
+          if (phase == COG_PHASE_MOVEMENT) {
+            q0 = (float)cardf(kRes0, c); q1 = (float)cardf(kRes1, c); q2 = (float)cardf(kRes2, c);
+          } else if (phase == COG_PHASE_BUYING) {
+            const uint32_t coin = cardf(kRes2, c);
+            q2 = q2 + (coin > 0 ? (float)coin : 0.5f);
+          }
+        }
+        if ((int)(meta >> 24) != ag) q0 = q1 = q2 = 0.f;   // a turn end (Player::end_turn)
+        ph = px & 0xffu;
+      }
+      s.info[i * COG_INFO_BYTES + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag] = (uint8_t)(infob >> (8 * ag));
+      const uint4 g0 = make_uint4(px, __float_as_uint(q0), __float_as_uint(q1), __float_as_uint(q2));
       MBits ba{xa.x, xa.y, xa.z};
       if ((int)(meta >> 24) == ag && (meta & kMetaStepped)) {   // the turn goes on: update_observation's
         const uint32_t phase = g0.x & 0xffu;               // heads of ag's stored mask
@@ -4207,6 +4235,7 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
     if (live) {
 #pragma unroll
       for (int p = 0; p < 4; p++) D.heads[p][l] = D.stbA[p][l];
+      reinterpret_cast<uint32_t *>(s.priv + i)[12] = infob;   // Info steps (a parked env's: as of the park)
     }
   }
   PH_FLUSH(s_glob);
@@ -4223,7 +4252,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   __shared__ TrioLds D;
   // (roles rotated per workgroup, so that a CU's two workgroups could not put both stepping waves
   // on one SIMD, measured the same: profiles/r04y_trio_role_rotation.txt)
-  const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform
+  const uint32_t rot = s.trio_rot == 1u ? blockIdx.x : s.trio_rot == 2u ? blockIdx.x >> 8 : s.trio_rot == 3u ? (blockIdx.x >> 8) << 1 : 0u;
+  const int role = __builtin_amdgcn_readfirstlane((int)(((threadIdx.x >> 6) + rot) & 3u));   // wave-uniform
   if (threadIdx.x < 64) D.flg[threadIdx.x] = 0u;
   if (threadIdx.x < kTrioCnts) D.cnt[threadIdx.x] = 0u;
   park_list_clear_other(s);
@@ -4621,6 +4651,16 @@ int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rn
     const int epw = kind == RK_TRIO ? trio_epw(s.n) : 64;
     const unsigned nb = blocks_for(s.n, epw);
     const dim3 g(nb), gf(fixup_grid(nb));
+    static const int jt_env = [] {                         // $COG_TRIO_JT = 0 / 1 overrides (A/B)
+      const char *e = getenv("COG_TRIO_JT");
+      return e && *e ? atoi(e) : -1;
+    }();
+    static const int rot_env = [] {                        // $COG_TRIO_ROT (A/B)
+      const char *e = getenv("COG_TRIO_ROT");
+      return e && *e ? atoi(e) : 0;
+    }();
+    sd.trio_rot = (uint32_t)rot_env;
+    sd.trio_jt = jt_env >= 0 ? (uint32_t)(jt_env != 0) : (nb <= 256u ? 1u : 0u);
     if (mask_source == MASK_STORED) {
       hipLaunchKernelGGL((k_env_rollout_duo<MASK_STORED>), g, dim3(128), 0, st, sd, steps, d_rng, d_actions);
       hipLaunchKernelGGL((k_env_fixup<MASK_STORED>), gf, dim3(64), 0, st, sd, steps, d_rng, d_actions, epw);
