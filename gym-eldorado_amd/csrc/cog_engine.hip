@@ -3740,7 +3740,7 @@ DEV void trio_store_private(const DevState &s, size_t i, const RegEnv &R, const 
   uint4 *pw = reinterpret_cast<uint4 *>(s.priv + i);
   reinterpret_cast<uint3 *>(reinterpret_cast<uint32_t *>(pw) + 1)[0] = make_uint3(R.seed, R.max_steps, R.turn_counter);
   pw[1] = make_uint4(R.g1x, R.g1y, R.in_market, R.flags);
-  s.heads[5 * i] = mbits_u4(selb);                         // (Info steps: storing wave A's)
+  s.heads[5 * i] = mbits_u4(selb);                         // (Info steps: the drawing wave's)
 }
 
 template <int SRC>
@@ -3808,6 +3808,15 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
   }
   PH(6);                                                   // the prologue (to the barrier)
   TrioCnt6 cc;
+  // step t + 1's presampled record, read at the end of step t when storing wave B is known to be
+  // past it (so that the read's latency overlaps the record's stores); else at step t + 1's start
+  uint3 pr_next = D.pre[0][l];
+  bool have_next = true;
+  // the next turn change's records read ahead (pf_ok: valid)
+  const bool tc_ahead = (s_glob.trio_pf & 2u) != 0u;
+  uint2 pf_hd = make_uint2(0u, 0u);
+  uint4 pf_pla = make_uint4(0u, 0u, 0u, 0u), pf_hdn = pf_pla;
+  bool pf_ok = false;
   for (int t = 0; t < steps; t++) {
     const int sl = t & (kTrioDepth - 1);
     if (t >= kTrioDepth) {                                 // slot t % kTrioDepth free
@@ -3815,13 +3824,13 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
       cnt_wait(D, cc, cc.stb, (uint32_t)(t - kTrioDepth + 1), s_glob);
     }
     PH(9);
-    if (t >= kTrioLead) cnt_wait(D, cc, cc.pre, (uint32_t)(t - kTrioLead + 1), s_glob);
+    if (!have_next) cnt_wait(D, cc, cc.pre, (uint32_t)(t - kTrioLead + 1), s_glob);   // (t >= kTrioLead)
     PH(2);
     bool ended = false, finish = false, turn_end = false, stepped = false;
     uint32_t a_play = 0u;
     if (live) {
       const uint32_t srng0 = srng;
-      const uint3 pr = D.pre[t & (kTrioLead - 1)][l];
+      const uint3 pr = have_next ? pr_next : D.pre[t & (kTrioLead - 1)][l];
       const bool fast = sample_lean(selb, pr, srng, a_play, s_glob.trio_jt != 0u, R.tab);
       bool other = false;                                  // an action head other than play set
       if (__builtin_amdgcn_ballot_w64(!fast) && !fast) {   // (wave-uniform skip)
@@ -3843,8 +3852,8 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
         park = (uint32_t)t | kParkRedo;
         live = false;
       } else if (!was_done) {                              // cog_env::step, the lean case
-        stepped = true;                                    // (Info steps and the resources: storing
-        uint32_t phase = R.sh[0] & 0xffu;                  // wave A's)
+        stepped = true;                                    // (Info steps and the resources: the
+        uint32_t phase = R.sh[0] & 0xffu;                  // drawing wave's)
         if (phase == COG_PHASE_INACTIVE) phase = COG_PHASE_MOVEMENT;
         steps_taken = (steps_taken + 1u) & 0xffu;
         if (a_play) {                                      // Player::play_card (player.cpp:45-60)
@@ -3892,14 +3901,16 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     // the new agent's records (hand, counters) and the next player's (stored mask), once the
     // drawing wave is past their last turn ends; read ahead of the record's stores, so that their
     // latency overlaps them
-    uint2 hd = make_uint2(0u, 0u);
-    uint4 pla = make_uint4(0u, 0u, 0u, 0u), hdn = pla;
-    if (__builtin_amdgcn_ballot_w64(tc)) {
+    // (read ahead at an earlier step of the turn when the drawing wave was past them: pf_ok)
+    uint2 hd = pf_hd;
+    uint4 pla = pf_pla, hdn = pf_hdn;
+    const bool slow = tc && !pf_ok;
+    if (__builtin_amdgcn_ballot_w64(slow)) {
       const int need = R.n_players() == 3u ? te1 : te2;   // the later of ag1's and na1's last turn ends
       // the drawing wave past record max(need) over the wave: its distance from t by ballots (no
       // cross-lane shuffles, which go through LDS); >= 2 in play (>= 3 players, turns of >= 2
       // steps), and from 5 on it asks for a little more than it needs
-      const bool w = tc && need >= 0;
+      const bool w = slow && need >= 0;
       if (__builtin_amdgcn_ballot_w64(w)) {
         int dmin = 5;
 #pragma unroll
@@ -3908,7 +3919,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
         cnt_wait(D, cc, cc.draw, (uint32_t)(t - dmin + 1), s_glob);
         PH(5);
       }
-      if (tc) {
+      if (slow) {
         hd = D.img[ag1][1][l];
         pla = D.pl[ag1][l];
         hdn = D.heads[na1][l];
@@ -3919,7 +3930,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
       if (tc || ended) D.pl[ag][l] = pack_lean_player(pp, n_in_hand, n_active, steps_taken);
       const uint32_t meta = kMetaValid | (uint32_t)ag << 2 | (uint32_t)na << 4 | (uint32_t)na1 << 6 |
                             (ended ? kMetaEnded : 0u) | (stepped ? kMetaStepped : 0u) | (uint32_t)ag1 << 24;
-      ring[0][l].x = R.sh[0];                              // (the resources: storing wave A's)
+      ring[0][l].x = R.sh[0];                              // (the resources: the drawing wave's)
       ring[1][l] = make_uint4(selb.w0, selb.w1, selb.w2, meta);
       ring[2][l] = make_uint4(stab.w0, stab.w1, stab.w2, a_play | (n_active & 0xffu) << 8);
       D.srng[sl][l] = srng;
@@ -3927,6 +3938,9 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
       ring[1][l] = make_uint4(0u, 0u, 0u, 0u);             // no record
     }
     cnt_store(D, CNT_REC, (uint32_t)(t + 1));
+    // (B rewrites slot (t + 1) % 4 only after record t + 1: this read is issued before that)
+    have_next = t + 1 < kTrioLead || ((s_glob.trio_pf & 1u) && cc.pre >= (uint32_t)(t + 2 - kTrioLead));
+    if (have_next) pr_next = D.pre[(t + 1) & (kTrioLead - 1)][l];
     PH(1);
     if (tc) {
       te2 = te1;
@@ -3944,6 +3958,19 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
 #pragma unroll
       for (int p = 2; p >= 0; p--) cn = na1 == p ? cells[p] : cn;
       cells_n = cn;
+      pf_ok = false;
+    }
+    // the next turn change's records (the agent after ag1 and the player after it), read ahead
+    // once the drawing wave is past their last turn ends (the counter as last read: no wait)
+    if (tc_ahead && live && !pf_ok && !ended) {
+      const int need = R.n_players() == 3u ? te1 : te2;   // (as the turn change itself will ask)
+      if (need < 0 || cc.draw >= (uint32_t)(need + 1)) {
+        const int nn = (int)next_player((uint32_t)na1, R.n_players());
+        pf_hd = D.img[na1][1][l];
+        pf_pla = D.pl[na1][l];
+        pf_hdn = D.heads[nn][l];
+        pf_ok = true;
+      }
     }
     if (live && ended) {                                   // hand the env to k_env_fixup
       trio_store_private(s, i, R, selb);
@@ -3987,6 +4014,8 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
   const bool live = l < epw && wbase + (size_t)l < s_glob.n;
   uint32_t rng = 0u;                                       // the env rng
   bool narrow = true;
+  uint4 shb0 = make_uint4(0u, 0u, 0u, 0u);                 // ObsData 16128.. as stored: the phase
+  uint32_t infob = 0u;                                     // dword and the resources; Info steps
   if (live) {
 #pragma unroll
     for (int p = 0; p < 4; p++) {
@@ -4000,6 +4029,8 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
       for (int q = 0; q < 5; q++) D.img[p][q][l] = pile[q];
     }
     rng = reinterpret_cast<const uint32_t *>(s.priv + i)[0];
+    infob = reinterpret_cast<const uint32_t *>(s.priv + i)[12];   // EnvPriv granule 3, dword 0
+    shb0 = reinterpret_cast<const uint4 *>(s.obs + i * COG_OBS_BYTES + COG_OBS_PHASE)[0];
   }
   D.wide[l] = narrow ? 0u : 1u;                            // (a wide env: the stepper parks it at step 0)
   uint32_t flags = 0u;                                     // hazard flags of the draws
@@ -4024,6 +4055,31 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
       agj[j] = ag;
       te[j] = rec && (int)(meta >> 24) != ag;
       const int a_play = (int)(D.ring[slot[j]][2][l].w & 0xffu);
+      if (live && (meta & kMetaValid)) {                   // the ObsData phase / resources granule and
+        uint4 g0 = shb0;                                   // the Info byte (the stepping wave leaves
+        if (rec) {                                         // the resources and the counts to this wave)
+          infob = (infob & ~(0xffu << (8 * ag))) | ((((infob >> (8 * ag)) + 1u) & 0xffu) << (8 * ag));
+          uint32_t phase = shb0.x & 0xffu;
+          if (phase == COG_PHASE_INACTIVE) phase = COG_PHASE_MOVEMENT;
+          if (a_play) {                                    // Player::play_card (player.cpp:45-60)
+            const int c = a_play - 1;
+            if (phase == COG_PHASE_MOVEMENT) {
+              g0.y = __float_as_uint((float)cardf(kRes0, c));
+              g0.z = __float_as_uint((float)cardf(kRes1, c));
+              g0.w = __float_as_uint((float)cardf(kRes2, c));
+            } else if (phase == COG_PHASE_BUYING) {
+              const uint32_t coin = cardf(kRes2, c);
+              g0.w = __float_as_uint(__uint_as_float(g0.w) + (coin > 0 ? (float)coin : 0.5f));
+            }
+          }
+          if (te[j]) g0.y = g0.z = g0.w = 0u;              // Player::end_turn (+0.f)
+          g0.x = D.ring[slot[j]][0][l].x;
+        }
+        reinterpret_cast<uint3 *>(&D.ring[slot[j]][0][l].y)[0] = make_uint3(g0.y, g0.z, g0.w);   // (storing wave A)
+        s.info[i * COG_INFO_BYTES + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag] = (uint8_t)(infob >> (8 * ag));
+        if (ne4(g0, shb0)) reinterpret_cast<uint4 *>(s.obs + i * COG_OBS_BYTES + COG_OBS_PHASE)[0] = g0;
+        shb0 = g0;
+      }
       if (rec && a_play) {                                 // Deck::activate (cards.cpp:242-253): hand[c]--,
         const int c = a_play - 1;                          // active[c]++ (u8; c < 8: the stepping wave
         uint8_t *ph = reinterpret_cast<uint8_t *>(&D.img[ag][1][l]) + c;   // parks any other type)
@@ -4065,7 +4121,10 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
     cnt_store(D, CNT_DRAW, (uint32_t)(r + nrec));
     PH(9);
   }
-  if (live) reinterpret_cast<uint32_t *>(s.priv + i)[0] = rng;   // the env rng after its last draws
+  if (live) {
+    reinterpret_cast<uint32_t *>(s.priv + i)[0] = rng;     // the env rng after its last draws
+    reinterpret_cast<uint32_t *>(s.priv + i)[12] = infob;  // Info steps (a parked env's: as of the park)
+  }
   PH_FLUSH(s_glob);
   return flags;
 }
@@ -4084,7 +4143,6 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
   const size_t i = (size_t)l;
   const bool live = l < epw && wbase + (size_t)l < s_glob.n;
   uint8_t *__restrict__ av = actions_glob + wbase * COG_ACTION_BYTES;
-  uint4 shb0 = make_uint4(0u, 0u, 0u, 0u);                 // A: ObsData 16128.. as stored
   MBits selb = {0u, 0u, 0u};                               // B: the selected mask as stored
   uint2 cells[4];                                          // A: every player's neighbourhood cache
   uint32_t out = ~0u;                                      // B: dones[i] | agent_selection[i] << 8 as stored
@@ -4092,14 +4150,9 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
   E.flags = 0u;
   E.avail = 0u;
   uint32_t x = 1u;                                         // B: the sampler state at step 0
-  uint32_t infob = 0u, ph = 0u;                            // A: Info steps (u8 per player), the phase
-  float q0 = 0.f, q1 = 0.f, q2 = 0.f;                      // A: and the resources before the record
   if (live) {
     if (PART == 0) {
       const uint4 *sh4 = reinterpret_cast<const uint4 *>(s.obs + i * COG_OBS_BYTES + COG_OBS_PHASE);
-      shb0 = sh4[0];
-      ph = shb0.x & 0xffu;
-      q0 = __uint_as_float(shb0.y); q1 = __uint_as_float(shb0.z); q2 = __uint_as_float(shb0.w);
       const uint4 sh1 = sh4[1], sh2 = sh4[2];
       const uint4 *pv4 = reinterpret_cast<const uint4 *>(s.priv + i);
 #pragma unroll
@@ -4108,7 +4161,6 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
         cells[p] = reinterpret_cast<const uint2 *>(pv4 + 8)[p];
       }
       const uint4 g1 = pv4[1];
-      infob = reinterpret_cast<const uint32_t *>(pv4 + 3)[0];   // EnvPriv granule 3, dword 0
       const uint32_t w[5] = {sh1.x, sh1.y, sh1.z, sh1.w, sh2.x};
       E.avail = shop_avail_of(w, (g1.y >> 8) & 0xffu, g1.z);   // (no purchase in the lean step: fixed)
     } else {
@@ -4167,26 +4219,7 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
     const bool rec = live && (meta & kMetaValid);
     const int ag = (int)((meta >> 2) & 3u), na = (int)((meta >> 4) & 3u);
     if (rec && PART == 0) {
-      const uint4 xa = D.ring[sl][2][l], oa = D.stbA[ag][l];
-      const uint32_t px = D.ring[sl][0][l].x;
-      if (meta & kMetaStepped) {                           // Info steps_taken (u8) and the step's
-        infob = (infob & ~(0xffu << (8 * ag))) | ((((infob >> (8 * ag)) + 1u) & 0xffu) << (8 * ag));
-        const uint32_t phase = ph == COG_PHASE_INACTIVE ? (uint32_t)COG_PHASE_MOVEMENT : ph;
-        const uint32_t a_play = xa.w & 0xffu;              // resources (the stepping wave leaves them)
-        if (a_play) {                                      // Player::play_card (player.cpp:45-60)
-          const int c = (int)a_play - 1;
-          if (phase == COG_PHASE_MOVEMENT) {
-            q0 = (float)cardf(kRes0, c); q1 = (float)cardf(kRes1, c); q2 = (float)cardf(kRes2, c);
-          } else if (phase == COG_PHASE_BUYING) {
-            const uint32_t coin = cardf(kRes2, c);
-            q2 = q2 + (coin > 0 ? (float)coin : 0.5f);
-          }
-        }
-        if ((int)(meta >> 24) != ag) q0 = q1 = q2 = 0.f;   // a turn end (Player::end_turn)
-        ph = px & 0xffu;
-      }
-      s.info[i * COG_INFO_BYTES + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag] = (uint8_t)(infob >> (8 * ag));
-      const uint4 g0 = make_uint4(px, __float_as_uint(q0), __float_as_uint(q1), __float_as_uint(q2));
+      const uint4 g0 = D.ring[sl][0][l], xa = D.ring[sl][2][l], oa = D.stbA[ag][l];
       MBits ba{xa.x, xa.y, xa.z};
       if ((int)(meta >> 24) == ag && (meta & kMetaStepped)) {   // the turn goes on: update_observation's
         const uint32_t phase = g0.x & 0xffu;               // heads of ag's stored mask
@@ -4199,9 +4232,6 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
         const uint32_t sp = phase == COG_PHASE_BUYING ? E.shop_bits(r2) : 1u;
         ba.w2 = (ba.w2 & ~kMoveShopBits) | mv << 2 | sp << 9;
       }
-      uint8_t *ob = s.obs + i * COG_OBS_BYTES;
-      if (ne4(g0, shb0)) reinterpret_cast<uint4 *>(ob + COG_OBS_PHASE)[0] = g0;
-      shb0 = g0;
       uint8_t *deck = deck_ptr(s, i, ag);
       store_mask_record(reinterpret_cast<uint4 *>(deck + COG_PD_MASK), ba, mask_diff_granules(ba, mbits_of(oa)));
       D.stbA[ag][l] = mbits_u4(ba);
@@ -4235,7 +4265,6 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
     if (live) {
 #pragma unroll
       for (int p = 0; p < 4; p++) D.heads[p][l] = D.stbA[p][l];
-      reinterpret_cast<uint32_t *>(s.priv + i)[12] = infob;   // Info steps (a parked env's: as of the park)
     }
   }
   PH_FLUSH(s_glob);
@@ -4660,6 +4689,11 @@ int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rn
       return e && *e ? atoi(e) : 0;
     }();
     sd.trio_rot = (uint32_t)rot_env;
+    static const int pf_env = [] {                         // $COG_TRIO_PF = 0: no read-ahead (A/B)
+      const char *e = getenv("COG_TRIO_PF");
+      return e && *e ? atoi(e) : 3;
+    }();
+    sd.trio_pf = (uint32_t)pf_env;
     sd.trio_jt = jt_env >= 0 ? (uint32_t)(jt_env != 0) : (nb <= 256u ? 1u : 0u);
     if (mask_source == MASK_STORED) {
       hipLaunchKernelGGL((k_env_rollout_duo<MASK_STORED>), g, dim3(128), 0, st, sd, steps, d_rng, d_actions);
