@@ -62,6 +62,8 @@ struct PhAcc {
 #define PH(k) do { const unsigned long long t_ = stamp_clock(); ph_.acc[k] += t_ - ph_.last; ph_.last = t_; } while (0)
 #define PH_PARAM , PhAcc &ph_
 #define PH_PASS , ph_
+// TL(k): slot k holds the chip-wide 100 MHz clock at this point (the launch timeline)
+#define TL(k) do { ph_.acc[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define PH_FLUSH(s)                                                                         \
   do {                                                                                      \
     if ((s).stamps && (threadIdx.x & 63) == 0)                                              \
@@ -74,6 +76,7 @@ struct PhAcc {
 #define PH_PARAM
 #define PH_PASS
 #define PH_FLUSH(s) do { } while (0)
+#define TL(k) do { } while (0)
 #endif
 
 namespace cog {
@@ -3670,17 +3673,20 @@ DEV bool compact_of(const uint4 dk[7], uint2 pile[5]) {
   uint32_t d[28];
 #pragma unroll
   for (int k = 0; k < 7; k++) { d[4 * k] = dk[k].x; d[4 * k + 1] = dk[k].y; d[4 * k + 2] = dk[k].z; d[4 * k + 3] = dk[k].w; }
-  uint32_t rest = 0u;                                      // every byte of types 8..20
+  uint32_t rest = 0u;                                      // every byte of types 8..20: one
+#pragma unroll                                             // compile-time byte mask per dword
+  for (int k = 0; k < 28; k++) {
+    uint32_t m = 0u;
+#pragma unroll
+    for (int y = 4 * k; y < 4 * k + 4; y++)
+      if (y < 105 && y % 21 >= 8) m |= 0xffu << (8 * (y & 3));
+    if (m) rest |= d[k] & m;
+  }
 #pragma unroll
   for (int p = 0; p < 5; p++) {
     const int b = 21 * p, q = b >> 2, sh = b & 3;
     pile[p].x = sh ? __builtin_amdgcn_alignbyte(d[q + 1], d[q], sh) : d[q];
     pile[p].y = sh ? __builtin_amdgcn_alignbyte(d[q + 2], d[q + 1], sh) : d[q + 1];
-#pragma unroll
-    for (int t = 8; t < 21; t++) {                         // bytes b + 8 .. b + 20
-      const int y = b + t;
-      rest |= (d[y >> 2] >> (8 * (y & 3))) & 0xffu;
-    }
   }
   return rest == 0u;
 }
@@ -3754,6 +3760,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
   bool live = l < ne;
   uint32_t park = kParkNone, srng = 0;
   PH_DECL;                                                 // (diagnostic builds: phase stamps)
+  TL(10);                                                  // (and the launch timeline: slots 10..14)
   RegEnv R;                                                // env level (the lean image below)
   uint2 cells[4];                                          // every player's neighbourhood cache
   // the steps of the last two turn ends before the current step (-1: none in this launch); the
@@ -3765,7 +3772,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
   MBits selb = {0u, 0u, 0u}, stab = selb, stnb = selb;     // selected, stored(ag), stored(na)
   uint4 pp = make_uint4(0u, 0u, 0u, 0u);                   // PlayerPriv of ag (packed)
   uint32_t n_in_hand = 0u, n_active = 0u, steps_taken = 0u;
-  uint2 cells_a = make_uint2(0u, 0u), cells_n = cells_a;   // ag's and na's neighbourhoods (the done check)
+  uint32_t own = 0u;                                       // each player's own hex code (a byte each)
   if (live) {
     Snap S;
     load_env(s, i, S);
@@ -3784,14 +3791,8 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     n_in_hand = (pp.y >> 8) & 0xffu;
     n_active = (pp.y >> 16) & 0xffu;
     steps_taken = (pp.z >> 8) & 0xffu;
-    uint2 ca = cells[3], cn = cells[3];                    // (selects: no indexed registers)
 #pragma unroll
-    for (int p = 2; p >= 0; p--) {
-      ca = ag == p ? cells[p] : ca;
-      cn = na == p ? cells[p] : cn;
-    }
-    cells_a = ca;
-    cells_n = cn;
+    for (int p = 0; p < 4; p++) own |= (cells[p].x & 0xffu) << (8 * p);   // (neighbourhood cell 0)
     selb = S.sel;
     stab = mbits_of(D.heads[ag][l]);
     stnb = mbits_of(D.heads[na][l]);
@@ -3807,6 +3808,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     lean_p = narrow && lean_player(pp);
   }
   PH(6);                                                   // the prologue (to the barrier)
+  TL(11);
   TrioCnt6 cc;
   // step t + 1's presampled record, read at the end of step t when storing wave B is known to be
   // past it (so that the read's latency overlaps the record's stores); else at step t + 1's start
@@ -3860,13 +3862,10 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
           const int c = (int)a_play - 1;
           const uint32_t prev = hand_take(H, c);           // Deck::activate's hand part (the active
           n_in_hand = (n_in_hand - 1u) & 0xffu;            // pile: the drawing wave, trio_drawer)
-          const bool pl = prev > 1u;
-          const uint32_t bp = 1u << (c + 1);              // the play bit; the special bit 23 + c
-          selb.w0 = pl ? (selb.w0 | bp) : (selb.w0 & ~bp);
-          const bool sp = pl && is_special(c);
-          const uint32_t bs0 = c <= 8 ? 1u << (23 + c) : 0u, bs1 = c >= 9 ? 1u << (c - 9) : 0u;
-          selb.w0 = sp ? (selb.w0 | bs0) : (selb.w0 & ~bs0);
-          selb.w1 = sp ? (selb.w1 | bs1) : (selb.w1 & ~bs1);
+          // the play bit (its special bit stays clear: types 0-7 are not special, is_special; a
+          // type >= 8 has parked above)
+          const uint32_t bp = 1u << (c + 1);
+          selb.w0 = prev > 1u ? (selb.w0 | bp) : (selb.w0 & ~bp);
           n_active = (n_active + 1u) & 0xffu;
           pp.z = (pp.z & ~0xffu) | (uint32_t)c;            // idx_last
         } else {
@@ -3882,10 +3881,10 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
           R.turn_counter++;
         }
         R.sh[0] = (R.sh[0] & ~0xffu) | phase;
-        // done (environment.cpp:183-207): the (next) agent's cell or the turn counter
-        const uint2 cc = turn_end ? cells_n : cells_a;
-        const uint32_t c0 = R.use_cell(cc, 0);
-        finish = COG_HEX_END(c0) || R.turn_counter >= R.max_steps;
+        // done (environment.cpp:183-207): the (next) agent's cell or the turn counter.  Both change
+        // only with the turn here (no move: the agent's cell is the one checked after its last
+        // step, never an end; a player's own cell is never an out-of-bounds lookup)
+        finish = turn_end && (COG_HEX_END((own >> (8 * na)) & 0xffu) || R.turn_counter >= R.max_steps);
         if (finish) R.set_done(1u);
         PH(0);
       }
@@ -3953,11 +3952,6 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
       lean_p = narrow && lean_player(pla);
       stab = stnb;
       stnb = mbits_of(hdn);
-      cells_a = cells_n;
-      uint2 cn = cells[3];                                 // (selects: no indexed registers)
-#pragma unroll
-      for (int p = 2; p >= 0; p--) cn = na1 == p ? cells[p] : cn;
-      cells_n = cn;
       pf_ok = false;
     }
     // the next turn change's records (the agent after ag1 and the player after it), read ahead
@@ -3983,9 +3977,11 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     PH(3);
   }
   if (live) D.pl[ag][l] = pack_lean_player(pp, n_in_hand, n_active, steps_taken);   // (the epilogue's)
+  TL(12);
   cnt_store(D, CNT_REC, (uint32_t)steps + 1u);             // the loop is over (storing wave A's epilogue)
   cnt_wait(D, cc, cc.fin, 3u, s_glob);                     // the other waves are done
   PH(7);                                                   // the drain (the other waves' last records)
+  TL(13);
   const uint32_t fl = D.flg[l];                            // their hazard flags
   if (live) {                                              // env-level private state back to HBM
     R.flags |= fl;
@@ -3998,6 +3994,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
   park_list_push(s_glob, park != kParkNone);
   trio_store_players(D, s, ne);                            // every player's records (cooperative)
   PH(8);                                                   // the epilogue's stores (issued)
+  TL(14);
   PH_FLUSH(s_glob);
 }
 
@@ -4042,6 +4039,7 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
     const int nrec = r + 1 < steps ? 2 : 1;
     cnt_wait(D, cc, cc.rec, (uint32_t)(r + nrec), s_glob);   // the records are written
     PH(8);
+    if (r + nrec >= steps) TL(11);                         // (timeline: the last records written)
     const int slot[2] = {r & (kTrioDepth - 1), (r + 1) & (kTrioDepth - 1)};
     uint32_t dm[2] = {0u, 0u};
     int agj[2] = {0, 0};
@@ -4121,6 +4119,7 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
     cnt_store(D, CNT_DRAW, (uint32_t)(r + nrec));
     PH(9);
   }
+  TL(12);
   if (live) {
     reinterpret_cast<uint32_t *>(s.priv + i)[0] = rng;     // the env rng after its last draws
     reinterpret_cast<uint32_t *>(s.priv + i)[12] = infob;  // Info steps (a parked env's: as of the park)
@@ -4183,6 +4182,24 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
   // stepping wave waits for them), and record r - kTrioBLag's deck granules once drawn, so that
   // the presampled draws never wait for the drawing wave.  A: record r once drawn.
   constexpr int LAG = PART == 1 ? kTrioBLag : 0;
+  auto deck_rec = [&](int q) {                             // B: the deck granules record q changed
+    const int sl = q & (kTrioDepth - 1);
+    const uint32_t meta = D.ring[sl][1][l].w;
+    const int ag = (int)((meta >> 2) & 3u);
+    if (live && (meta & kMetaValid)) {                     // (from img)
+      const uint32_t dm = D.ring[sl][2][l].w >> 16;
+      uint2 pile[5];
+#pragma unroll
+      for (int k = 0; k < 5; k++) pile[k] = D.img[ag][k][l];
+      uint4 dk[7];
+      deck_expand(pile, dk);
+      uint4 *deck = reinterpret_cast<uint4 *>(deck_ptr(s, i, ag));
+#pragma unroll
+      for (int k = 0; k < 7; k++)
+        if ((dm >> k) & 1u) deck[k] = dk[k];
+    }
+    cnt_store(D, CNT_STB, (uint32_t)(q + 1));
+  };
   TrioCnt6 cc;
   for (int r = 0; r < steps + LAG; r++) {
     if (PART == 1 && r < steps) {                          // record r written
@@ -4215,6 +4232,7 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
     const int sl = q & (kTrioDepth - 1);
     cnt_wait(D, cc, cc.draw, (uint32_t)(q + 1), s_glob);
     PH(6);
+    if (q == steps - 1) TL(11);                            // (timeline: the last record drawn)
     const uint32_t meta = D.ring[sl][1][l].w;
     const bool rec = live && (meta & kMetaValid);
     const int ag = (int)((meta >> 2) & 3u), na = (int)((meta >> 4) & 3u);
@@ -4243,21 +4261,14 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
         D.stbA[na][l] = mbits_u4(bn);
       }
     }
-    if (rec && PART == 1) {                                // deck granules the record changed, from img
-      const uint32_t dm = D.ring[sl][2][l].w >> 16;
-      uint2 pile[5];
-#pragma unroll
-      for (int q = 0; q < 5; q++) pile[q] = D.img[ag][q][l];
-      uint4 dk[7];
-      deck_expand(pile, dk);
-      uint4 *deck = reinterpret_cast<uint4 *>(deck_ptr(s, i, ag));
-#pragma unroll
-      for (int k = 0; k < 7; k++)
-        if ((dm >> k) & 1u) deck[k] = dk[k];
+    if (PART == 1) {
+      deck_rec(q);
+    } else {
+      cnt_store(D, CNT_STA, (uint32_t)(q + 1));
     }
-    cnt_store(D, PART == 0 ? CNT_STA : CNT_STB, (uint32_t)(q + 1));
     PH(13);
   }
+  TL(12);
   // A: the stored-mask bit vectors as stored (the epilogue's; the drawing wave's turn ends
   // included), once the stepping wave no longer reads them
   if (PART == 0) {

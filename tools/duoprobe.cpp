@@ -106,6 +106,34 @@ int main(int argc, char **argv) {
         for (int k = 0; k < 10; k++) printf("%s\"%s\": %.1f", k ? ", " : "", trio_step_names[k], ph[k]);
         printf("}}\n");
       }
+      if (wpg == 4) {                                      // the launch timeline (stepping waves, 100 MHz)
+        unsigned long long t0 = ~0ull;
+        for (size_t w = 0; w < waves; w += wpg) t0 = std::min(t0, h[w * K + 10]);
+        const char *tl_names[5] = {"stepper start (after the table barrier)", "prologue done (barrier B)",
+                                   "last step done", "other waves done (FIN)", "epilogue stores issued"};
+        printf("  launch timeline of a %d-step launch (us after the first stepper start; median / max over workgroups):\n", chunk);
+        for (int k = 10; k < 15; k++) {
+          std::vector<double> v;
+          for (size_t w = 0; w < waves; w += wpg) v.push_back((double)(h[w * K + k] - t0) * 0.01);
+          const double mx = *std::max_element(v.begin(), v.end());
+          printf("    %-42s %8.2f %8.2f\n", tl_names[k - 10], med(v), mx);
+        }
+        const char *rn[4] = {"", "drawing", "storing A", "storing B"};
+        for (int role = 1; role < 4; role++)
+          for (int k = 11; k < 13; k++) {
+            std::vector<double> v;
+            for (size_t w = role; w < waves; w += wpg) v.push_back((double)(h[w * K + k] - t0) * 0.01);
+            printf("    %-10s %-31s %8.2f %8.2f\n", rn[role], k == 11 ? "last record's wait returned" : "loop done",
+                   med(v), *std::max_element(v.begin(), v.end()));
+          }
+        printf("TIMELINE_JSON {\"envs\": %zu, \"steps\": %d", n, chunk);
+        for (int k = 10; k < 15; k++) {
+          std::vector<double> v;
+          for (size_t w = 0; w < waves; w += wpg) v.push_back((double)(h[w * K + k] - t0) * 0.01);
+          printf(", \"t%d_med\": %.2f, \"t%d_max\": %.2f", k - 10, med(v), k - 10, *std::max_element(v.begin(), v.end()));
+        }
+        printf("}\n");
+      }
       for (int role = 0; role < wpg; role++) {
         const char **pn = role == 0 ? (wpg == 4 ? trio_step_names : step_names)
                                     : (wpg == 4 && role == 1) ? draw_names : store_names;
