@@ -64,6 +64,7 @@ struct PhAcc {
 #define PH_PASS , ph_
 // TL(k): slot k holds the chip-wide 100 MHz clock at this point (the launch timeline)
 #define TL(k) do { ph_.acc[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define PH_RESET do { ph_.last = stamp_clock(); } while (0)
 #define PH_FLUSH(s)                                                                         \
   do {                                                                                      \
     if ((s).stamps && (threadIdx.x & 63) == 0)                                              \
@@ -77,6 +78,7 @@ struct PhAcc {
 #define PH_PASS
 #define PH_FLUSH(s) do { } while (0)
 #define TL(k) do { } while (0)
+#define PH_RESET do { } while (0)
 #endif
 
 namespace cog {
@@ -3611,7 +3613,7 @@ DEV void cnt_wait(TrioLds &D, TrioCnt6 &c, const uint32_t &field, uint32_t v, co
       c.abort = 1u;
       return;
     }
-    __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_s_sleep(2);                           // (1 or 0: the same, r05y2)
   }
 }
 // the stepping wave's presampled record: {the state the step starts from, head 0's index for every
@@ -3799,6 +3801,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
   }
   R.tab = D.tab;
   __builtin_amdgcn_s_waitcnt(0);                           // (no per-iteration vmcnt wait covers them)
+  TL(15);                                                  // (timeline: this wave's prologue done)
   __syncthreads();                                         // B: every wave's prologue is done
   uint2 H = make_uint2(0u, 0u);                            // ag's hand (compact: types 0-7)
   bool lean_p = false, narrow = false;
@@ -4004,6 +4007,8 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
 // duo_turn_end: the env rng is this wave's).  Which granules each record changed goes to storing
 // wave B (ring granule 2, bits 16..22).
 DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw) {
+  PH_DECL;
+  TL(14);                                                  // (timeline: this wave's start)
   const int l = (int)(threadIdx.x & 63);
   const size_t wbase = (size_t)blockIdx.x * epw;
   const DevState s = wave_view(s_glob, wbase);
@@ -4032,8 +4037,9 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
   D.wide[l] = narrow ? 0u : 1u;                            // (a wide env: the stepper parks it at step 0)
   uint32_t flags = 0u;                                     // hazard flags of the draws
   __builtin_amdgcn_s_waitcnt(0);
+  TL(15);                                                  // (timeline: this wave's prologue done)
   __syncthreads();                                         // B: the decks are in LDS
-  PH_DECL;
+  PH_RESET;
   TrioCnt6 cc;
   for (int r = 0; r < steps; r += 2) {
     const int nrec = r + 1 < steps ? 2 : 1;
@@ -4136,6 +4142,8 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
 template <int PART>
 DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw, const uint32_t *__restrict__ rngs_glob,
                          uint8_t *__restrict__ actions_glob) {
+  PH_DECL;
+  TL(14);                                                  // (timeline: this wave's start)
   const int l = (int)(threadIdx.x & 63);
   const size_t wbase = (size_t)blockIdx.x * epw;
   const DevState s = wave_view(s_glob, wbase);
@@ -4176,8 +4184,9 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
     }
   }
   __builtin_amdgcn_s_waitcnt(0);
+  TL(15);                                                  // (timeline: this wave's prologue done)
   __syncthreads();                                         // B
-  PH_DECL;
+  PH_RESET;
   // B runs two cursors: record r's part that needs no draws (the presampled draws first: the
   // stepping wave waits for them), and record r - kTrioBLag's deck granules once drawn, so that
   // the presampled draws never wait for the drawing wave.  A: record r once drawn.

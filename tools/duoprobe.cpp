@@ -118,7 +118,13 @@ int main(int argc, char **argv) {
           const double mx = *std::max_element(v.begin(), v.end());
           printf("    %-42s %8.2f %8.2f\n", tl_names[k - 10], med(v), mx);
         }
-        const char *rn[4] = {"", "drawing", "storing A", "storing B"};
+        const char *rn[4] = {"stepping", "drawing", "storing A", "storing B"};
+        for (int role = 0; role < 4; role++) {
+          std::vector<double> v;
+          for (size_t w = role; w < waves; w += wpg) v.push_back((double)(h[w * K + 15] - t0) * 0.01);
+          printf("    %-10s %-31s %8.2f %8.2f\n", rn[role], "prologue loads done", med(v),
+                 *std::max_element(v.begin(), v.end()));
+        }
         for (int role = 1; role < 4; role++)
           for (int k = 11; k < 13; k++) {
             std::vector<double> v;
