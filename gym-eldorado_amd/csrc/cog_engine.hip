@@ -3751,7 +3751,7 @@ DEV void trio_store_private(const DevState &s, size_t i, const RegEnv &R, const 
   s.heads[5 * i] = mbits_u4(selb);                         // (Info steps: the drawing wave's)
 }
 
-template <int SRC>
+template <int SRC, bool LAT>
 DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, uint32_t *__restrict__ rngs_glob) {
   const int l = (int)(threadIdx.x & 63);
   const size_t wbase = (size_t)blockIdx.x * epw;
@@ -3772,6 +3772,11 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
   int te1 = -1, te2 = -1;
   int ag = 0, na = 0;
   MBits selb = {0u, 0u, 0u}, stab = selb, stnb = selb;     // selected, stored(ag), stored(na)
+  // The acting player's counters (steps_taken, n_in_hand, n_active, idx_last) are kept by this
+  // wave and handed to the drawing wave at turn changes when two workgroups share a CU (their
+  // total work per CU counts), and by the drawing wave alone when a workgroup has its CU to
+  // itself (LAT: the stepping wave's chain counts): profiles/r05_trio_ab.txt r05z3 / r05z5
+  constexpr bool lat = LAT;
   uint4 pp = make_uint4(0u, 0u, 0u, 0u);                   // PlayerPriv of ag (packed)
   uint32_t n_in_hand = 0u, n_active = 0u, steps_taken = 0u;
   uint32_t own = 0u;                                       // each player's own hex code (a byte each)
@@ -3836,7 +3841,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     if (live) {
       const uint32_t srng0 = srng;
       const uint3 pr = have_next ? pr_next : D.pre[t & (kTrioLead - 1)][l];
-      const bool fast = sample_lean(selb, pr, srng, a_play, s_glob.trio_jt != 0u, R.tab);
+      const bool fast = sample_lean(selb, pr, srng, a_play, LAT, R.tab);
       bool other = false;                                  // an action head other than play set
       if (__builtin_amdgcn_ballot_w64(!fast) && !fast) {   // (wave-uniform skip)
         uint8_t act[5];
@@ -3853,30 +3858,33 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
         srng = srng0;
         trio_store_private(s, i, R, selb);
         rngs[i] = srng;
-        D.pl[ag][l] = pack_lean_player(pp, n_in_hand, n_active, steps_taken);   // (the epilogue's)
+        if (!lat) D.pl[ag][l] = pack_lean_player(pp, n_in_hand, n_active, steps_taken);   // (the epilogue's)
         park = (uint32_t)t | kParkRedo;
         live = false;
       } else if (!was_done) {                              // cog_env::step, the lean case
         stepped = true;                                    // (Info steps and the resources: the
         uint32_t phase = R.sh[0] & 0xffu;                  // drawing wave's)
         if (phase == COG_PHASE_INACTIVE) phase = COG_PHASE_MOVEMENT;
-        steps_taken = (steps_taken + 1u) & 0xffu;
+        if (!lat) steps_taken = (steps_taken + 1u) & 0xffu;
         if (a_play) {                                      // Player::play_card (player.cpp:45-60)
           const int c = (int)a_play - 1;
           const uint32_t prev = hand_take(H, c);           // Deck::activate's hand part (the active
-          n_in_hand = (n_in_hand - 1u) & 0xffu;            // pile: the drawing wave, trio_drawer)
+                                                           // pile and the counters: the drawing wave)
           // the play bit (its special bit stays clear: types 0-7 are not special, is_special; a
           // type >= 8 has parked above)
           const uint32_t bp = 1u << (c + 1);
           selb.w0 = prev > 1u ? (selb.w0 | bp) : (selb.w0 & ~bp);
-          n_active = (n_active + 1u) & 0xffu;
-          pp.z = (pp.z & ~0xffu) | (uint32_t)c;            // idx_last
+          if (!lat) {
+            n_in_hand = (n_in_hand - 1u) & 0xffu;
+            n_active = (n_active + 1u) & 0xffu;
+            pp.z = (pp.z & ~0xffu) | (uint32_t)c;          // idx_last
+          }
         } else {
           phase = phase == COG_PHASE_BUYING ? COG_PHASE_INACTIVE : phase + 1u;   // pass: next phase
         }
         turn_end = phase == COG_PHASE_INACTIVE;            // maybe_end_turn -> next_agent
-        if (turn_end) {
-          n_active = 0u;                                   // Player::end_turn (the deck: drawing wave)
+        if (turn_end) {                                    // (Player::end_turn: the drawing wave)
+          n_active = 0u;
           stab = selb;                                     // save_actionmask
           R.set_agent((uint32_t)na);
           selb = stnb;                                     // load_actionmask (na != ag: >= 3 players)
@@ -3928,13 +3936,12 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
       }
     }
     if (live) {
-      // the acting player's counters: the drawing wave's at its turn end, the epilogue's at a park
-      if (tc || ended) D.pl[ag][l] = pack_lean_player(pp, n_in_hand, n_active, steps_taken);
+      if (!lat && (tc || ended)) D.pl[ag][l] = pack_lean_player(pp, n_in_hand, n_active, steps_taken);
       const uint32_t meta = kMetaValid | (uint32_t)ag << 2 | (uint32_t)na << 4 | (uint32_t)na1 << 6 |
                             (ended ? kMetaEnded : 0u) | (stepped ? kMetaStepped : 0u) | (uint32_t)ag1 << 24;
       ring[0][l].x = R.sh[0];                              // (the resources: the drawing wave's)
       ring[1][l] = make_uint4(selb.w0, selb.w1, selb.w2, meta);
-      ring[2][l] = make_uint4(stab.w0, stab.w1, stab.w2, a_play | (n_active & 0xffu) << 8);
+      ring[2][l] = make_uint4(stab.w0, stab.w1, stab.w2, a_play | (lat ? 0u : (n_active & 0xffu) << 8));
       D.srng[sl][l] = srng;
     } else {
       ring[1][l] = make_uint4(0u, 0u, 0u, 0u);             // no record
@@ -3979,22 +3986,39 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     na = na1;
     PH(3);
   }
-  if (live) D.pl[ag][l] = pack_lean_player(pp, n_in_hand, n_active, steps_taken);   // (the epilogue's)
   TL(12);
+  if (live && !lat) D.pl[ag][l] = pack_lean_player(pp, n_in_hand, n_active, steps_taken);   // (the epilogue's)
   cnt_store(D, CNT_REC, (uint32_t)steps + 1u);             // the loop is over (storing wave A's epilogue)
+  // the env-level private state back to HBM (lat: while the other waves drain; the flags word after
+  // them: it takes their hazard flags); no other wave reads these words in the launch
+  uint4 *pw = reinterpret_cast<uint4 *>(s.priv + i);
+  if (lat) {
+    if (live) {
+      reinterpret_cast<uint3 *>(reinterpret_cast<uint32_t *>(pw) + 1)[0] = make_uint3(R.seed, R.max_steps, R.turn_counter);
+      s.heads[5 * i] = mbits_u4(selb);
+      rngs[i] = srng;
+    }
+    if (l < ne) s.park[i] = park;
+    park_list_push(s_glob, park != kParkNone);
+  }
   cnt_wait(D, cc, cc.fin, 3u, s_glob);                     // the other waves are done
   PH(7);                                                   // the drain (the other waves' last records)
   TL(13);
   const uint32_t fl = D.flg[l];                            // their hazard flags
-  if (live) {                                              // env-level private state back to HBM
-    R.flags |= fl;
-    trio_store_private(s, i, R, selb);
-    rngs[i] = srng;
-  } else if (l < ne && fl) {                               // a parked env: flags of its last records
-    reinterpret_cast<uint32_t *>(s.priv + i)[7] = R.flags | fl;
+  if (lat) {
+    if (live) pw[1] = make_uint4(R.g1x, R.g1y, R.in_market, R.flags | fl);
+    else if (l < ne && fl) reinterpret_cast<uint32_t *>(pw)[7] = R.flags | fl;   // a parked env: its last records'
+  } else {
+    if (live) {
+      R.flags |= fl;
+      trio_store_private(s, i, R, selb);
+      rngs[i] = srng;
+    } else if (l < ne && fl) {
+      reinterpret_cast<uint32_t *>(pw)[7] = R.flags | fl;
+    }
+    if (l < ne) s.park[i] = park;
+    park_list_push(s_glob, park != kParkNone);
   }
-  if (l < ne) s.park[i] = park;
-  park_list_push(s_glob, park != kParkNone);
   trio_store_players(D, s, ne);                            // every player's records (cooperative)
   PH(8);                                                   // the epilogue's stores (issued)
   TL(14);
@@ -4006,6 +4030,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
 // Deck::activate does); then one pass over the turn ends of either record (discard + draws,
 // duo_turn_end: the env rng is this wave's).  Which granules each record changed goes to storing
 // wave B (ring granule 2, bits 16..22).
+template <bool LAT>
 DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw) {
   PH_DECL;
   TL(14);                                                  // (timeline: this wave's start)
@@ -4016,6 +4041,7 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
   const bool live = l < epw && wbase + (size_t)l < s_glob.n;
   uint32_t rng = 0u;                                       // the env rng
   bool narrow = true;
+  constexpr bool lat = LAT;                                // (the acting player's counters: trio_stepper)
   uint4 shb0 = make_uint4(0u, 0u, 0u, 0u);                 // ObsData 16128.. as stored: the phase
   uint32_t infob = 0u;                                     // dword and the resources; Info steps
   if (live) {
@@ -4047,9 +4073,9 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
     PH(8);
     if (r + nrec >= steps) TL(11);                         // (timeline: the last records written)
     const int slot[2] = {r & (kTrioDepth - 1), (r + 1) & (kTrioDepth - 1)};
-    uint32_t dm[2] = {0u, 0u};
+    uint32_t dm[2] = {0u, 0u}, nact[2] = {0u, 0u};
     int agj[2] = {0, 0};
-    bool te[2] = {false, false};
+    bool te[2] = {false, false}, recj[2] = {false, false};
 #pragma unroll
     for (int j = 0; j < 2; j++) {                          // the plays, in record order
       if (j >= nrec) continue;                             // (uniform)
@@ -4057,8 +4083,23 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
       const int ag = (int)((meta >> 2) & 3u);
       const bool rec = live && (meta & kMetaValid) && (meta & kMetaStepped);
       agj[j] = ag;
+      recj[j] = rec;
       te[j] = rec && (int)(meta >> 24) != ag;
       const int a_play = (int)(D.ring[slot[j]][2][l].w & 0xffu);
+      if (rec && lat) {                                    // the acting player's counters (PlayerPriv:
+        uint4 p4 = D.pl[ag][l];                            // steps_taken, n_in_hand, n_active, idx_last;
+        uint32_t na = (p4.y >> 16) & 0xffu;                // Player::play_card, player.cpp:45-60; u8)
+        p4.z = (p4.z & 0xffff00ffu) | (((p4.z >> 8) + 1u) & 0xffu) << 8;
+        if (a_play) {
+          p4.y = (p4.y & 0xffff00ffu) | ((((p4.y >> 8) & 0xffu) - 1u) & 0xffu) << 8;
+          na = (na + 1u) & 0xffu;
+          p4.z = (p4.z & ~0xffu) | (uint32_t)(a_play - 1);
+        }
+        if (te[j]) na = 0u;                                // Player::end_turn
+        p4.y = (p4.y & 0xff00ffffu) | na << 16;
+        D.pl[ag][l] = p4;
+        nact[j] = na;
+      }
       if (live && (meta & kMetaValid)) {                   // the ObsData phase / resources granule and
         uint4 g0 = shb0;                                   // the Info byte (the stepping wave leaves
         if (rec) {                                         // the resources and the counts to this wave)
@@ -4118,10 +4159,12 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
       dm[1] |= j == 1 ? dd : 0u;
     }
 #pragma unroll
-    for (int j = 0; j < 2; j++)                            // (bytes 14..15 of granule 2: its last dword's
-      if (j < nrec)                                        // upper half; the action and n_active below are
-                                                           // the stepping wave's)
-        reinterpret_cast<uint16_t *>(&D.ring[slot[j]][2][l])[7] = (uint16_t)dm[j];
+    for (int j = 0; j < 2; j++)                            // granule 2's last dword: the action (the
+      if (j < nrec) {                                      // stepping wave's), n_active, the changed deck
+        uint32_t *w = &D.ring[slot[j]][2][l].w;            // granules (storing waves A and B)
+        if (lat && recj[j]) *w = (*w & 0xffu) | nact[j] << 8 | dm[j] << 16;
+        else reinterpret_cast<uint16_t *>(w)[1] = (uint16_t)dm[j];
+      }
     cnt_store(D, CNT_DRAW, (uint32_t)(r + nrec));
     PH(9);
   }
@@ -4139,7 +4182,7 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
 // lean step leaves them) -- and wave B (PART 1) the presampled draws (presample), the
 // selected-mask record, the Info steps byte, the action, dones / agent_selection and the decks.
 // Each keeps its own images of what it stored last.
-template <int PART>
+template <int PART, bool LAT>
 DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw, const uint32_t *__restrict__ rngs_glob,
                          uint8_t *__restrict__ actions_glob) {
   PH_DECL;
@@ -4179,7 +4222,7 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
 #pragma unroll
     for (int k = 0; k < kTrioLead; k++) {
       const uint4 p = presample(x);
-      D.pre[k][l] = pre_pack(p, s_glob.trio_jt != 0u);
+      D.pre[k][l] = pre_pack(p, LAT);
       x = p.z;
     }
   }
@@ -4219,7 +4262,7 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
       const uint32_t meta = m.w;
       const bool rec = live && (meta & kMetaValid);
       if (rec && r + kTrioLead < steps)                    // step r + 4's draws: the state after step r,
-        D.pre[(r + kTrioLead) & (kTrioLead - 1)][l] = pre_pack(presample(mr_jump(D.srng[sl][l], kPow15)), s_glob.trio_jt != 0u);
+        D.pre[(r + kTrioLead) & (kTrioLead - 1)][l] = pre_pack(presample(mr_jump(D.srng[sl][l], kPow15)), LAT);
       cnt_store(D, CNT_PRE, (uint32_t)(r + 1));            // + 15 draws (steps r + 1 .. r + 3)
       const uint32_t a_play = D.ring[sl][2][l].w & 0xffu;
       if (rec) {
@@ -4295,7 +4338,10 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
 // epw.. idle (trio_epw: half-empty waves fill all 256 CUs at 8,192 envs).  The drawing and storing
 // waves leave their hazard flags in flg[] and count themselves done in cnt[FIN]; the stepping wave
 // waits for all three before its epilogue.
-template <int SRC>
+// LAT (a launch of at most one workgroup per CU, DevState::trio_jt): head 0's index table in the
+// presampled records and the acting player's counters on the drawing wave -- the stepping wave's
+// chain is the launch's time; otherwise (two workgroups share a CU) the total work per CU counts
+template <int SRC, bool LAT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_env_rollout_trio(DevState s, int steps, int epw, uint32_t *__restrict__ rngs,
                                                           uint8_t *__restrict__ actions_out) {
   __shared__ TrioLds D;
@@ -4309,13 +4355,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   uid_tab_fill(D.tab);                                     // (ends on a barrier)
   if (role == 0) {
     __builtin_amdgcn_s_setprio(3);
-    trio_stepper<SRC>(D, s, steps, epw, rngs);
+    trio_stepper<SRC, LAT>(D, s, steps, epw, rngs);
     return;
   }
   uint32_t flags;
-  if (role == 1) flags = trio_drawer(D, s, steps, epw);
-  else if (role == 2) flags = trio_storer<0>(D, s, steps, epw, rngs, actions_out);
-  else flags = trio_storer<1>(D, s, steps, epw, rngs, actions_out);
+  if (role == 1) flags = trio_drawer<LAT>(D, s, steps, epw);
+  else if (role == 2) flags = trio_storer<0, LAT>(D, s, steps, epw, rngs, actions_out);
+  else flags = trio_storer<1, LAT>(D, s, steps, epw, rngs, actions_out);
   const int l = (int)(threadIdx.x & 63);
   if (flags) __hip_atomic_fetch_or(&D.flg[l], flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   if (l == 0) __hip_atomic_fetch_add(&D.cnt[CNT_FIN], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -4722,8 +4768,12 @@ int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rn
       // (k_env_fixup inside the trio launch, for shards of one workgroup per CU -- inlined, or as a
       // never-inlined call -- was slower: 20-step launch at 8,192 44.2 / 42.0 against 41.3 us,
       // profiles/r04t_trio_fused.txt)
-      hipLaunchKernelGGL((k_env_rollout_trio<MASK_SELECTED>), g, dim3(256), trio_pad_lds(nb), st, sd, steps, epw, d_rng,
-                         d_actions);
+      if (sd.trio_jt)
+        hipLaunchKernelGGL((k_env_rollout_trio<MASK_SELECTED, true>), g, dim3(256), trio_pad_lds(nb), st, sd, steps, epw,
+                           d_rng, d_actions);
+      else
+        hipLaunchKernelGGL((k_env_rollout_trio<MASK_SELECTED, false>), g, dim3(256), trio_pad_lds(nb), st, sd, steps, epw,
+                           d_rng, d_actions);
       if (!sd.no_fixup)
         hipLaunchKernelGGL((k_env_fixup<MASK_SELECTED>), gf, dim3(64), 0, st, sd, steps, d_rng, d_actions, epw);
     } else {
