@@ -114,10 +114,7 @@ struct DevState {
   uint32_t *parkq;
   uint32_t park_par;
   uint32_t no_fixup;                 // 1: no k_env_fixup follows this launch (a park is an error)
-  uint32_t trio_jt;                  // 1: the trio's presampled records carry head 0's index table
-  uint32_t trio_rot;                 // (A/B) trio role rotation by workgroup
-  uint32_t trio_pf;                  // (A/B) the stepping wave's read-ahead: 1 the next presampled
-                                     // record, 2 the next turn change's records
+  uint32_t trio_jt;                  // 1: the trio launch of at most one workgroup per CU (its LAT form)
   // direct publish (launch_step_pub only; null otherwise): device addresses of the shard's pinned
   // ObsData view and outs block, and the publish mirror (k_publish's `mir`)
   uint8_t *pub_obs, *pub_outs, *pub_mir;

@@ -3823,7 +3823,6 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
   uint3 pr_next = D.pre[0][l];
   bool have_next = true;
   // the next turn change's records read ahead (pf_ok: valid)
-  const bool tc_ahead = (s_glob.trio_pf & 2u) != 0u;
   uint2 pf_hd = make_uint2(0u, 0u);
   uint4 pf_pla = make_uint4(0u, 0u, 0u, 0u), pf_hdn = pf_pla;
   bool pf_ok = false;
@@ -3948,7 +3947,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     }
     cnt_store(D, CNT_REC, (uint32_t)(t + 1));
     // (B rewrites slot (t + 1) % 4 only after record t + 1: this read is issued before that)
-    have_next = t + 1 < kTrioLead || ((s_glob.trio_pf & 1u) && cc.pre >= (uint32_t)(t + 2 - kTrioLead));
+    have_next = t + 1 < kTrioLead || cc.pre >= (uint32_t)(t + 2 - kTrioLead);
     if (have_next) pr_next = D.pre[(t + 1) & (kTrioLead - 1)][l];
     PH(1);
     if (tc) {
@@ -3966,7 +3965,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     }
     // the next turn change's records (the agent after ag1 and the player after it), read ahead
     // once the drawing wave is past their last turn ends (the counter as last read: no wait)
-    if (tc_ahead && live && !pf_ok && !ended) {
+    if (live && !pf_ok && !ended) {
       const int need = R.n_players() == 3u ? te1 : te2;   // (as the turn change itself will ask)
       if (need < 0 || cc.draw >= (uint32_t)(need + 1)) {
         const int nn = (int)next_player((uint32_t)na1, R.n_players());
@@ -4346,9 +4345,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
                                                           uint8_t *__restrict__ actions_out) {
   __shared__ TrioLds D;
   // (roles rotated per workgroup, so that a CU's two workgroups could not put both stepping waves
-  // on one SIMD, measured the same: profiles/r04y_trio_role_rotation.txt)
-  const uint32_t rot = s.trio_rot == 1u ? blockIdx.x : s.trio_rot == 2u ? blockIdx.x >> 8 : s.trio_rot == 3u ? (blockIdx.x >> 8) << 1 : 0u;
-  const int role = __builtin_amdgcn_readfirstlane((int)(((threadIdx.x >> 6) + rot) & 3u));   // wave-uniform
+  // on one SIMD, measured the same: profiles/r04y_trio_role_rotation.txt, r05_trio_ab.txt r05s)
+  const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform
   if (threadIdx.x < 64) D.flg[threadIdx.x] = 0u;
   if (threadIdx.x < kTrioCnts) D.cnt[threadIdx.x] = 0u;
   park_list_clear_other(s);
@@ -4750,16 +4748,6 @@ int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rn
       const char *e = getenv("COG_TRIO_JT");
       return e && *e ? atoi(e) : -1;
     }();
-    static const int rot_env = [] {                        // $COG_TRIO_ROT (A/B)
-      const char *e = getenv("COG_TRIO_ROT");
-      return e && *e ? atoi(e) : 0;
-    }();
-    sd.trio_rot = (uint32_t)rot_env;
-    static const int pf_env = [] {                         // $COG_TRIO_PF = 0: no read-ahead (A/B)
-      const char *e = getenv("COG_TRIO_PF");
-      return e && *e ? atoi(e) : 3;
-    }();
-    sd.trio_pf = (uint32_t)pf_env;
     sd.trio_jt = jt_env >= 0 ? (uint32_t)(jt_env != 0) : (nb <= 256u ? 1u : 0u);
     if (mask_source == MASK_STORED) {
       hipLaunchKernelGGL((k_env_rollout_duo<MASK_STORED>), g, dim3(128), 0, st, sd, steps, d_rng, d_actions);
