@@ -3520,20 +3520,23 @@ __global__ void __launch_bounds__(128) k_env_rollout_duo(DevState s, int steps, 
 //                  cnt[STB] = r + 1
 //   storing wave A record r once drawn: ObsData, the stored masks; cnt[STA] = r + 1
 // The waits form no cycle: every wait of the stepping wave needs only records it has published.
-// A wait that outlasts kTrioSpinLimit polls (a bug, never a slow wave) sets F_SYNC_TIMEOUT and the
-// host error word and goes on, so that no fault can hang the GPU.
+// A wait that outlasts kTrioSpinLimit polls (a bug, never a slow wave) sets F_SYNC_TIMEOUT, the
+// host error word and a sticky abort counter that ends every wait of the workgroup, so that no
+// fault can hang the GPU.
 //
-// record t: 0 ObsData 16128.. (phase, resources; the lean step never changes the shop), 1 selected-
-// mask bits + meta, 2 the acting player's stored-mask bits (saved mask at a turn end: the drawing
-// wave adds the drawn cards) + action byte 0 + n_active of the acting player << 8 + the deck
+// record t: 0 ObsData 16128.. (the phase dword from the stepping wave; the resources from the
+// drawing wave; the lean step never changes the shop), 1 selected-mask bits + meta, 2 the acting
+// player's stored-mask bits (saved mask at a turn end: the drawing wave adds the drawn cards) +
+// action byte 0 + n_active of the acting player << 8 (the drawing wave's in the LAT form) + the deck
 // granules the record changed << 16 (drawing wave).  The next player's stored mask changes only at a
 // turn end, by fixed heads (the lean step), so storing wave A derives it from its own image.  The
 // neighbourhood caches never change in the lean step (no moves): the stepping wave and storing wave
-// A keep their own copies, and the epilogue does not store them.  The stepping wave's player
-// counters go to LDS only at a turn end (the drawing wave's) and at a park or the end (the epilogue's).
+// A keep their own copies, and the epilogue does not store them.  The acting player's counters: the
+// stepping wave's, written to LDS at a turn end (for the drawing wave) and at a park or the end (for
+// the epilogue); in the LAT form the drawing wave's alone.
 constexpr int kTrioRingG = 3;
-#ifndef COG_TRIO_DEPTH                                     // (diagnostic builds: tools/r04/gpu_depth.sh)
-#define COG_TRIO_DEPTH 8                                   // (16 measured the same: profiles/r05i_trio_depth16.txt)
+#ifndef COG_TRIO_DEPTH                                     // (diagnostic builds)
+#define COG_TRIO_DEPTH 8                                   // (16 measured the same: profiles/r05i_trio_depth16.txt, r05_trio_ab.txt r05z7)
 #endif
 constexpr int kTrioDepth = COG_TRIO_DEPTH;                 // ring slots (records in flight)
 constexpr int kTrioLead = 4;                               // presampled draws: steps ahead of the record
@@ -4028,7 +4031,9 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
 // each record's play replayed on the acting player's deck (the hand and active piles, as
 // Deck::activate does); then one pass over the turn ends of either record (discard + draws,
 // duo_turn_end: the env rng is this wave's).  Which granules each record changed goes to storing
-// wave B (ring granule 2, bits 16..22).
+// wave B (ring granule 2, bits 16..22).  It also stores each record's ObsData phase/resources
+// granule and Info steps byte (the resources for storing wave A in ring granule 0), and with LAT
+// keeps the acting player's counters (PlayerPriv: steps_taken, n_in_hand, n_active, idx_last).
 template <bool LAT>
 DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw) {
   PH_DECL;
@@ -4176,11 +4181,11 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
   return flags;
 }
 
-// The store phase of the trio on two waves: wave A (PART 0) the ObsData shared block and the
-// stored masks -- update_observation's heads of the acting player's when the turn goes on (the
-// lean step leaves them) -- and wave B (PART 1) the presampled draws (presample), the
-// selected-mask record, the Info steps byte, the action, dones / agent_selection and the decks.
-// Each keeps its own images of what it stored last.
+// The store phase of the trio on two waves: wave A (PART 0) the stored masks --
+// update_observation's heads of the acting player's when the turn goes on (the lean step leaves
+// them) -- and wave B (PART 1) the presampled draws (presample; with LAT head 0's index table), the
+// selected-mask record, the action, dones / agent_selection and the decks.  Each keeps its own
+// images of what it stored last.
 template <int PART, bool LAT>
 DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw, const uint32_t *__restrict__ rngs_glob,
                          uint8_t *__restrict__ actions_glob) {
