@@ -170,10 +170,15 @@ def load_profile():
         return None
 
 
-def make(cg, n, base, device, difficulty=None, max_steps=MAX_STEPS, device_views=True, stored=False):
+def make(cg, n, seed, device, difficulty=None, max_steps=MAX_STEPS, device_views=True, stored=False, first=0):
+    """The batch of global envs [first, first + n) of a run seeded `seed`: env i reset with
+    (u32)(seed + first + i) (vec_environment.h:41), sampler i seeded seed + first + i unwrapped
+    (vec_sampler.h:9-13), so that a rank's shard equals the same envs of one unsharded batch."""
+    from city_of_gold.shard import shard_seed
     env = cg.vec.get_vec_env(n)(device=device)
-    smp = cg.vec.get_vec_sampler(n)(base, device=device)
-    env.reset(base, N_PLAYERS, N_PIECES, cg.HARD if difficulty is None else difficulty, max_steps, False)
+    smp = cg.vec.get_vec_sampler(n)(seed, device=device, first_index=first)
+    env.reset(shard_seed(seed, first), N_PLAYERS, N_PIECES, cg.HARD if difficulty is None else difficulty,
+              max_steps, False)
     runner = cg.vec.get_runner(n)(env, smp, None, device_views=device_views, stored_masks=stored)
     return env, smp, runner
 
@@ -521,15 +526,14 @@ def main():
     args = parse()
     d = Dist(args.gpus)
     import city_of_gold as cg
-    from city_of_gold.shard import shard, shard_seed
+    from city_of_gold.shard import shard
 
     dev = device_of(d)
     bind_device(d, dev)
     lo, hi = shard(args.envs_total, d.rank, d.world)       # env i of rank r = global index lo + i
     n = hi - lo
-    base = shard_seed(SEED, lo)
     t0 = time.time()
-    env, smp, runner = make(cg, n, base, dev)
+    env, smp, runner = make(cg, n, SEED, dev, first=lo)
     setup_s = time.time() - t0
     chunk = max(1, min(args.chunk, max(args.steps, 1)))
     runner.set_chunk(chunk)
@@ -628,7 +632,7 @@ def main():
                             "algorithmic_bytes_per_launch": ENCODE_BYTES * n}
         del runner, smp, env
         # full dynamics: stored masks (moves, shop, specials), episodes of 30 turns -> auto-resets
-        env, smp, runner = make(cg, n, base, dev, max_steps=30, stored=True)
+        env, smp, runner = make(cg, n, SEED, dev, max_steps=30, stored=True, first=lo)
         runner.set_chunk(500)
         runner.rollout(200)
         d.barrier_sync(runner)
@@ -647,7 +651,7 @@ def main():
         del runner, smp, env
         # full dynamics without the constant resets: stored masks, max_steps 100,000 (episodes of the
         # reference harness's length), 1,000-step launches -- the general step's own rate
-        env, smp, runner = make(cg, n, base, dev, stored=True)
+        env, smp, runner = make(cg, n, SEED, dev, stored=True, first=lo)
         runner.set_chunk(1000)
         runner.rollout(200)
         d.barrier_sync(runner)

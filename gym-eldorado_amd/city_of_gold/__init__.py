@@ -13,7 +13,8 @@ Differences, all additive: any N is accepted (the reference stops at 256 and onl
 N in {0..8, 16, 32, ..., 256}); input arrays are length/record-size checked (ValueError instead
 of an out-of-bounds read); views keep their owner alive.  Runners accept two extra keyword
 arguments: device_views=True keeps outputs in HBM (no per-sync host copy) and
-stored_masks=True samples from the current agent's stored mask (full game dynamics).
+stored_masks=True samples from the current agent's stored mask (full game dynamics); samplers
+accept first_index= for a rank's block of a larger batch (city_of_gold.shard).
 
 All computation runs in libcog_hip.so on a gfx950 GPU.  There is no CPU fallback: creating an
 environment without a usable device raises RuntimeError.
@@ -87,8 +88,11 @@ def _make_env_cls(n):
 
 
 def _make_sampler_cls(n):
-    def __init__(self, seed=None, device=None):
-        _C.VecSamplerBase.__init__(self, n, seed, device)
+    def __init__(self, seed=None, device=None, *, first_index=0):
+        """first_index (an addition): the batch is envs [first_index, first_index + n) of a larger
+        one (a rank's shard, city_of_gold.shard), so sampler i is seeded seed + first_index + i
+        unwrapped, as in the whole batch (vec_sampler.h:9-13)."""
+        _C.VecSamplerBase.__init__(self, n, seed, device, first_index)
 
     return type(VEC_SAMPLER_CLS + str(n), (_C.VecSamplerBase,), {"__init__": __init__,
                                                                  "__module__": "city_of_gold.vec.env"})

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -295,7 +296,8 @@ struct cog_env {
   size_t n = 0;
   uint8_t n_players = 4;              // the batch's players (reset params; the default ctor's 4)
   uint32_t max_steps = 0;             // the last reset's max_steps (0: unknown)
-  uint64_t version = 0;               // calls that changed the env state so far (SamplerSpec)
+  uint64_t version = 0;               // changes of the env state (SamplerSpec): from a process-wide
+                                      // counter, so no two envs ever share a version value
   std::vector<EnvShard> sh;
   uint32_t *h_err = nullptr;          // pinned, device-mapped: one error word per shard (256 B apart)
   // host views: obs is one pinned allocation; the small records are the shard's h_outs block
@@ -366,6 +368,12 @@ namespace {
 
 bool single(const cog_env *e) { return e->sh.size() == 1; }
 
+// cog_env::version: every change of any env's state takes the next value of one process-wide
+// counter (with per-env counters starting at 0, an env allocated at a freed env's
+// address could reach the version a stale speculation recorded)
+std::atomic<uint64_t> g_env_versions{0};
+void env_changed(cog_env *e) { e->version = g_env_versions.fetch_add(1, std::memory_order_relaxed) + 1; }
+
 // Envs with host views, for cog_sampler_sample: when the masks it gets are one env shard's own
 // pinned selected-mask view on the sampler shard's device, and that shard's views equal HBM
 // (host_synced: its last publish stored them), the sampler reads the same records in HBM instead
@@ -416,6 +424,14 @@ bool env_stream_in_flight(const EnvShard &k) { return k.pub_done || k.done.queue
 void env_free(cog_env *e) {
   if (!e) return;
   host_env_register(e, false);
+  {                                                        // a speculation on this env is void: a new
+    std::lock_guard<std::mutex> lk(g_host_envs_mu);        // env at the same address must not match it
+    for (cog_sampler *q : g_samplers)
+      if (q->spec.env == e) {
+        q->spec.ok = false;
+        q->spec.env = nullptr;
+      }
+  }
   for (EnvShard &k : e->sh) {
     DeviceGuard g(k.device);
     if (k.stream) (void)hipStreamSynchronize(k.stream);
@@ -737,6 +753,7 @@ int cog_env_create_multi(size_t n_envs, const int *devices, int n_devices, cog_e
   if (rc) return rc;
   cog_env *e = new cog_env();
   e->n = n_envs;
+  env_changed(e);
   const size_t err_bytes = 64 * sizeof(uint32_t) * (size_t)n_devices;
   if ((rc = hmalloc(&e->h_err, err_bytes, hipHostMallocMapped | hipHostMallocCoherent))) {
     env_free(e);
@@ -793,7 +810,7 @@ int cog_env_shard_info(const cog_env *env, int k, size_t *first, size_t *count, 
 static int env_reset_impl(cog_env *e, const cog::ResetParams &p) {
   int rc = prepare_host(e);
   if (rc) return rc;
-  e->version++;
+  env_changed(e);
   if (p.use_params) {
     e->n_players = p.n_players;
     e->max_steps = p.max_steps;
@@ -851,7 +868,7 @@ int cog_env_step_device_stream(cog_env *env, const void *d_actions, size_t n, vo
   DeviceGuard g(k.device);
   int rc = prepare_host(env);
   if (rc) return rc;
-  env->version++;
+  env_changed(env);
   if (stream != COG_NO_STREAM) {      // the caller's stream produced the actions: order after it
     HIPCHK(hipEventRecord(k.ev, static_cast<hipStream_t>(stream)));   // (NULL: the null stream)
     HIPCHK(hipStreamWaitEvent(k.stream, k.ev, 0));
@@ -885,7 +902,7 @@ int cog_env_step(cog_env *env, const cog_action_t *actions, size_t n) {
   if (n != env->n) return fail(COG_ERR_INVALID, "actions length != num_envs");
   int rc = prepare_host(env);
   if (rc) return rc;
-  env->version++;
+  env_changed(env);
   // the actions are a sampler's own view: its next sample, speculatively (SamplerSpec)
   cog_sampler *q = single(env) && n ? sampler_of_actions(actions, n) : nullptr;
   if (q && (q->exported || q->sh[0].device != env->sh[0].device || std::getenv("COG_NO_SPEC") || !spec_ready(q)))
@@ -1161,7 +1178,7 @@ int cog_env_set_autoreset(cog_env *env, int on) {
   if (!env) return fail(COG_ERR_INVALID, "env is NULL");
   int rc = sync_all(env);
   if (rc) return rc;
-  env->version++;
+  env_changed(env);
   for (EnvShard &k : env->sh) {
     k.s.autoreset = on ? 1u : 0u;
     k.lean_clock = ~0ull;
@@ -1171,6 +1188,11 @@ int cog_env_set_autoreset(cog_env *env, int on) {
 
 // ---- sampler -----------------------------------------------------------------------------
 int cog_sampler_create_multi(size_t n_envs, uint64_t seed, const int *devices, int n_devices, cog_sampler **out) {
+  return cog_sampler_create_at(n_envs, seed, 0, devices, n_devices, out);
+}
+
+int cog_sampler_create_at(size_t n_envs, uint64_t seed, uint64_t first_index, const int *devices, int n_devices,
+                          cog_sampler **out) {
   if (!out) return fail(COG_ERR_INVALID, "out is NULL");
   *out = nullptr;
   int rc = check_devices(devices, n_devices);
@@ -1209,10 +1231,11 @@ int cog_sampler_create_multi(size_t n_envs, uint64_t seed, const int *devices, i
       k.done.h = s->h_sig + 64 * j;
       k.done.d = static_cast<uint32_t *>(d_sig);
     }
-    // vec_action_sampler(seed) (vec_sampler.h:9-13): sampler i seeded seed + i, seed a u32
+    // vec_action_sampler(seed) (vec_sampler.h:9-13): sampler i seeded seed + i, seed a u32, the sum
+    // in size_t; i is the global index first_index + k.first + j
     if (hipMemsetAsync(k.d_actions, 0, k.n * COG_ACTION_BYTES, k.stream) != hipSuccess ||
         hipMemsetAsync(k.done.ctr, 0, 256, k.stream) != hipSuccess ||
-        cog::launch_seed_sampler(k.n, (uint64_t)(uint32_t)seed, k.first, k.d_rng, k.stream)) {
+        cog::launch_seed_sampler(k.n, (uint64_t)(uint32_t)seed, (size_t)first_index + k.first, k.d_rng, k.stream)) {
       sampler_free(s);
       return fail(COG_ERR_HIP, "sampler init failed");
     }
@@ -1414,7 +1437,7 @@ static void views_pending(EnvShard &k) {
 
 static int runner_launch_fused(cog_runner *r, int steps) {
   const int src = (r->flags & COG_RUNNER_STORED_MASKS) ? cog::MASK_STORED : cog::MASK_SELECTED;
-  r->env->version++;
+  env_changed(r->env);
   r->smp->version++;
   const bool host = runner_host(r);
   int rc;
@@ -1484,7 +1507,7 @@ int cog_runner_sample(cog_runner *r) {
 
 int cog_runner_step(cog_runner *r) {
   if (!r) return fail(COG_ERR_INVALID, "runner is NULL");
-  r->env->version++;
+  env_changed(r->env);
   if (r->pending_sample) {
     r->pending_sample = false;
     return runner_launch_fused(r, 1);

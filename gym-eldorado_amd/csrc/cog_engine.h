@@ -118,10 +118,12 @@ struct DevState {
   // direct publish (launch_step_pub only; null otherwise): device addresses of the shard's pinned
   // ObsData view and outs block, and the publish mirror (k_publish's `mir`)
   uint8_t *pub_obs, *pub_outs, *pub_mir;
-  // test hook ($COG_DEBUG_REDO_STEP, launch_rollout): the duo rollout's deferred turn end parks
-  // every env at this step of each launch as if its action drew from the env rng (kParkRedo), so
-  // the tests exercise that path; -1 (default): off
+  // test hooks (launch_rollout): the trio parks every env (redo_env -1: $COG_DEBUG_REDO_STEP) or
+  // the env of local index redo_env ($COG_DEBUG_PARK_NOFIX=t:i, with no_fixup kept) at step
+  // redo_at of each launch as if its action left the lean step (kParkRedo), so the tests exercise
+  // the fix-up's redo path and the no-fix-up guard (F_PARK_NOFIX); redo_at -1 (default): off
   int32_t redo_at;
+  int64_t redo_env;
 };
 
 struct ResetParams {

@@ -3856,7 +3856,7 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
       const bool was_done = R.done() != 0u;
       // not the lean step's case (never in the canonical loop), or the test hook: hand the env to
       // k_env_fixup before its step t
-      if (!was_done && (!lean_p || other || t == s.redo_at)) {
+      if (!was_done && (!lean_p || other || (t == s.redo_at && (s.redo_env < 0 || (int64_t)(wbase + i) == s.redo_env)))) {
         srng = srng0;
         trio_store_private(s, i, R, selb);
         rngs[i] = srng;
@@ -4708,26 +4708,47 @@ int trio_epw(size_t n) {
 // one per CU 5.43: profiles/r05f_trio_wpc.txt).  So a launch of more than one workgroup per CU
 // pads each workgroup's LDS to half a CU's (the dispatcher would otherwise pack three on some CUs);
 // $COG_TRIO_WPC = 1..4 overrides (A/B).
+// The current device's CU count and LDS bytes per CU (hipGetDeviceProperties once per device: a
+// partitioned MI355X exposes fewer CUs than the whole chip's 256; 160 KiB of LDS per CU on gfx950)
+struct CuShape {
+  unsigned cus;
+  size_t lds;
+};
+static CuShape cu_shape() {
+  static CuShape cache[64] = {};
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return {256u, 163840};
+  if (!cache[d].cus) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, d) == hipSuccess && p.multiProcessorCount > 0)
+      cache[d] = {(unsigned)p.multiProcessorCount,
+                  p.maxSharedMemoryPerMultiProcessor ? (size_t)p.maxSharedMemoryPerMultiProcessor : (size_t)163840};
+    else
+      cache[d] = {256u, 163840};
+  }
+  return cache[d];
+}
 static size_t trio_pad_lds(unsigned nblocks) {
   static const int forced = [] {
     const char *e = getenv("COG_TRIO_WPC");
     return e && *e ? atoi(e) : 0;
   }();
-  const int wpc = forced >= 1 && forced <= 4 ? forced : (nblocks > 256u ? 2 : 0);
+  const CuShape c = cu_shape();
+  const int wpc = forced >= 1 && forced <= 4 ? forced : (nblocks > c.cus ? 2 : 0);
   if (!wpc) return 0;
-  const size_t per = (size_t)163840 / (size_t)wpc - 2048;  // (a margin for the allocation granule)
+  const size_t per = c.lds / (size_t)wpc - 2048;           // (a margin for the allocation granule)
   return per > sizeof(TrioLds) ? per - sizeof(TrioLds) : 0;
 }
 // k_env_fixup's grid: at most this many one-wave workgroups stride over the parked list
 // ($COG_FIXUP_GRID overrides; A/B only).  A wave per CU keeps a launch with every workgroup parked
 // (short episodes) running in parallel, and a launch with none parked cheap.
 static unsigned fixup_grid(unsigned nblocks) {
-  static const unsigned cap = [] {
+  static const unsigned forced = [] {
     const char *e = getenv("COG_FIXUP_GRID");
     const int v = e && *e ? atoi(e) : 0;
-    return v > 0 ? (unsigned)v : 256u;
+    return v > 0 ? (unsigned)v : 0u;
   }();
-  return std::max(1u, std::min(nblocks, cap));
+  return std::max(1u, std::min(nblocks, forced ? forced : cu_shape().cus));
 }
 int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rng, uint8_t *d_actions, void *stream,
                    bool defer_ok, uint32_t *park_seq, bool no_fixup) {
@@ -4740,12 +4761,21 @@ int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rn
       const char *e = getenv("COG_DEBUG_REDO_STEP");
       return e && *e ? atoi(e) : -1;
     }();
+    // test hook: "t:i" parks env i (local index) at step t of each launch and keeps a no-fix-up
+    // launch so (the guard's test: the park must surface as F_PARK_NOFIX)
+    static const std::pair<int, long long> park_nofix = [] {
+      const char *e = getenv("COG_DEBUG_PARK_NOFIX");
+      if (!e || !*e) return std::make_pair(-1, -1LL);
+      const char *c = strchr(e, ':');
+      return std::make_pair(atoi(e), c ? atoll(c + 1) : 0LL);
+    }();
     DevState sd = s;
-    sd.redo_at = redo_at;
+    sd.redo_at = park_nofix.first >= 0 ? park_nofix.first : redo_at;
+    sd.redo_env = park_nofix.first >= 0 ? (int64_t)park_nofix.second : -1;
     sd.park_par = (*park_seq)++ & 1u;
-    // (the test hook parks every env: never without the fix-up; $COG_ALWAYS_FIXUP for A/B)
+    // (the redo hook parks every env: never without the fix-up; $COG_ALWAYS_FIXUP for A/B)
     static const bool always_fixup = getenv("COG_ALWAYS_FIXUP") != nullptr;
-    sd.no_fixup = no_fixup && kind == RK_TRIO && redo_at < 0 && !always_fixup ? 1u : 0u;
+    sd.no_fixup = no_fixup && kind == RK_TRIO && (redo_at < 0 || park_nofix.first >= 0) && !always_fixup ? 1u : 0u;
     const int epw = kind == RK_TRIO ? trio_epw(s.n) : 64;
     const unsigned nb = blocks_for(s.n, epw);
     const dim3 g(nb), gf(fixup_grid(nb));
@@ -4753,7 +4783,7 @@ int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rn
       const char *e = getenv("COG_TRIO_JT");
       return e && *e ? atoi(e) : -1;
     }();
-    sd.trio_jt = jt_env >= 0 ? (uint32_t)(jt_env != 0) : (nb <= 256u ? 1u : 0u);
+    sd.trio_jt = jt_env >= 0 ? (uint32_t)(jt_env != 0) : (nb <= cu_shape().cus ? 1u : 0u);
     if (mask_source == MASK_STORED) {
       hipLaunchKernelGGL((k_env_rollout_duo<MASK_STORED>), g, dim3(128), 0, st, sd, steps, d_rng, d_actions);
       hipLaunchKernelGGL((k_env_fixup<MASK_STORED>), gf, dim3(64), 0, st, sd, steps, d_rng, d_actions, epw);

@@ -253,10 +253,10 @@ class VecEnv {
 // ---- vec sampler (py_vec_action_sampler, vectorized.h:107-127) ----------------------------
 class VecSampler {
  public:
-  VecSampler(size_t n, std::optional<size_t> seed, const py::object &device) : n_(n) {
+  VecSampler(size_t n, std::optional<size_t> seed, const py::object &device, uint64_t first_index) : n_(n) {
     const uint32_t s = (uint32_t)seed.value_or(std::random_device{}());   // u32 as in vectorized.h:113
     const std::vector<int> d = devices_of(device, n);
-    check(cog_sampler_create_multi(n, s, d.data(), (int)d.size(), &h_));
+    check(cog_sampler_create_at(n, s, first_index, d.data(), (int)d.size(), &h_));
   }
   ~VecSampler() { cog_sampler_destroy(h_); }
   VecSampler(const VecSampler &) = delete;
@@ -468,8 +468,8 @@ PYBIND11_MODULE(_city_of_gold, m) {
       }, "iters"_a = 20, "variant"_a = 0);
 
   py::class_<VecSampler>(m, "VecSamplerBase", py::dynamic_attr())
-      .def(py::init<size_t, std::optional<size_t>, const py::object &>(), "n_envs"_a, "seed"_a = py::none(),
-           "device"_a = py::none())
+      .def(py::init<size_t, std::optional<size_t>, const py::object &, uint64_t>(), "n_envs"_a, "seed"_a = py::none(),
+           "device"_a = py::none(), "first_index"_a = 0)
       .def("get_actions", [](py::object self) {
         VecSampler &s = self.cast<VecSampler &>();
         return view(s.actions(), s.num_envs(), self, true);   // an input of env.step: writable

@@ -174,6 +174,12 @@ COG_API int cog_sampler_create(size_t n_envs, uint64_t seed, int device, cog_sam
 /* sharded like cog_env_create_multi (a runner needs the env's and the sampler's shards equal) */
 COG_API int cog_sampler_create_multi(size_t n_envs, uint64_t seed, const int *devices, int n_devices,
                                      cog_sampler **out);
+/* the batch is the block [first_index, first_index + n_envs) of a larger one (a rank's shard,
+ * city_of_gold/shard.py): sampler i seeded seed + first_index + i, the sum in 64 bits as the
+ * unsharded batch computes it (vec_sampler.h:9-13), so a sharded run samples the same actions for
+ * every seed -- a u32 base of seed + first_index would wrap where the reference does not */
+COG_API int cog_sampler_create_at(size_t n_envs, uint64_t seed, uint64_t first_index, const int *devices,
+                                  int n_devices, cog_sampler **out);
 COG_API int cog_sampler_num_shards(const cog_sampler *s, int *out);
 COG_API void cog_sampler_destroy(cog_sampler *s);
 /* vec_action_sampler::sample(masks) (vec_sampler.h:14-21): n == num_envs host ActionMask

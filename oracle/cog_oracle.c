@@ -969,15 +969,18 @@ struct orc_sampler {
   cog_action_t *actions;
 };
 
-orc_sampler *orc_sampler_create(size_t n, uint32_t seed) {
+/* sampler i seeded seed + first + i in size_t (vec_sampler.h:9-13: seed + i, seed a u32; first: the
+   global index of env 0 when the batch is one rank's block of a larger one) */
+orc_sampler *orc_sampler_create_at(size_t n, uint32_t seed, uint64_t first) {
   orc_sampler *s = (orc_sampler *)calloc(1, sizeof(orc_sampler));
   s->n = n;
   s->rng = (uint32_t *)calloc(n + 1, sizeof(uint32_t));
   s->actions = (cog_action_t *)aligned_alloc(64, n * sizeof(cog_action_t) + 64);
   memset(s->actions, 0, n * sizeof(cog_action_t));
-  for (size_t i = 0; i < n; i++) s->rng[i] = mr_seed((uint64_t)seed + (uint64_t)i);
+  for (size_t i = 0; i < n; i++) s->rng[i] = mr_seed((uint64_t)seed + first + (uint64_t)i);
   return s;
 }
+orc_sampler *orc_sampler_create(size_t n, uint32_t seed) { return orc_sampler_create_at(n, seed, 0); }
 void orc_sampler_destroy(orc_sampler *s) {
   if (!s) return;
   free(s->rng); free(s->actions); free(s);

@@ -59,6 +59,7 @@ void orc_clear_flags(orc_vec *v);
 int orc_debug_state(const orc_vec *v, size_t i, uint32_t *out, size_t n_out);
 
 orc_sampler *orc_sampler_create(size_t n, uint32_t seed);
+orc_sampler *orc_sampler_create_at(size_t n, uint32_t seed, uint64_t first);   /* seeds seed + first + i */
 void orc_sampler_destroy(orc_sampler *s);
 void orc_sample(orc_sampler *s, const void *masks);   /* ActionMask[n] -> actions */
 void orc_sample_range(orc_sampler *s, const void *masks, size_t lo, size_t hi);

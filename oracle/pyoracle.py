@@ -129,6 +129,8 @@ class _Lib:
             lib.orc_debug_state.argtypes = [vp, sz, C.POINTER(C.c_uint32), sz]
             lib.orc_sampler_create.restype = vp
             lib.orc_sampler_create.argtypes = [sz, C.c_uint32]
+            lib.orc_sampler_create_at.restype = vp
+            lib.orc_sampler_create_at.argtypes = [sz, C.c_uint32, C.c_uint64]
             lib.orc_sampler_destroy.argtypes = [vp]
             lib.orc_sample.argtypes = [vp, vp]
             lib.orc_sampler_actions.restype = vp
@@ -229,10 +231,12 @@ class OracleVec:
 
 
 class OracleSampler:
-    def __init__(self, n, seed):
+    """vec_action_sampler(seed): sampler i seeded seed + first + i in size_t (vec_sampler.h:9-13);
+    first is the global index of env 0 when the batch is one rank's block of a larger batch."""
+    def __init__(self, n, seed, first=0):
         self.lib = _Lib.oracle()
         self.n = n
-        self.h = self.lib.orc_sampler_create(n, seed & 0xFFFFFFFF)
+        self.h = self.lib.orc_sampler_create_at(n, seed & 0xFFFFFFFF, first)
         self.actions = _view(self.lib.orc_sampler_actions(self.h), ACTION, (n,))
 
     def get_actions(self):

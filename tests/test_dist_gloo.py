@@ -27,27 +27,32 @@ def digests(vec, smp, lo, hi):
                            vec.infos[i:i + 1], smp.actions[i:i + 1]) for i in range(lo, hi)]
 
 
-def rollout(n, seed, steps):
+def rollout(n, seed, steps, first=0, sampler_seed=None):
+    """Envs [first, first + n) of a batch seeded `seed`: env reset seed (u32)(seed + first)
+    (shard_seed), sampler seeds seed + first + i unwrapped (first_index); sampler_seed replaces
+    the sampler's (seed, first) by (sampler_seed, 0) -- the wrapped base a rank used to pass."""
     import pyoracle as po
-    vec, smp = po.OracleVec(n), po.OracleSampler(n, seed)
-    vec.reset(seed, 4, 3, 2, 30)
+    from city_of_gold.shard import shard_seed
+    vec = po.OracleVec(n)
+    smp = po.OracleSampler(n, seed, first) if sampler_seed is None else po.OracleSampler(n, sampler_seed)
+    vec.reset(shard_seed(seed, first), 4, 3, 2, 30)
     for _ in range(steps):
         smp.sample(po.stored_masks(vec))
         vec.step(smp.actions)
     return digests(vec, smp, 0, n)
 
 
-def worker(rank, world, port, root, q):
+def worker(rank, world, port, root, q, n_total=N_TOTAL, seed=SEED, steps=STEPS):
     import sys
     for p in (os.path.join(root, "gym-eldorado_amd"), os.path.join(root, "oracle"), root):
         sys.path.insert(0, p)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import bench
-    from city_of_gold.shard import shard, shard_seed
+    from city_of_gold.shard import shard
     d = bench.Dist(world)
-    lo, hi = shard(N_TOTAL, rank, world)
-    mine = rollout(hi - lo, shard_seed(SEED, lo), STEPS)
+    lo, hi = shard(n_total, rank, world)
+    mine = rollout(hi - lo, seed, steps, first=lo)
     gathered = [None] * world
     d.dist.all_gather_object(gathered, (lo, [x.hex() for x in mine]))
     class _Runner:                                         # (no GPU: sync() stands in for the engine's)
@@ -67,25 +72,47 @@ def worker(rank, world, port, root, q):
     d.close()
 
 
-@pytest.mark.timeout(300)
-def test_two_rank_shards_equal_single_process():
+def run_two_ranks(n_total, seed, steps):
+    """gloo world 2: the gathered per-env digests of both ranks' shards, in global order"""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=worker, args=(r, 2, port, root, q)) for r in range(2)]
+    procs = [ctx.Process(target=worker, args=(r, 2, port, root, q, n_total, seed, steps)) for r in range(2)]
     for p in procs:
         p.start()
     gathered, mx, tot = q.get(timeout=240)
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    assert mx == 2.0 and tot == N_TOTAL
-    full = [x.hex() for x in rollout(N_TOTAL, SEED, STEPS)]
+    assert mx == 2.0 and tot == n_total
     merged = []
     for lo, ds in sorted(gathered):
         merged.extend(ds)
+    return merged
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_shards_equal_single_process():
+    merged = run_two_ranks(N_TOTAL, SEED, STEPS)
+    assert merged == [x.hex() for x in rollout(N_TOTAL, SEED, STEPS)]
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_shards_seed_exact_past_u32():
+    """Base seed 2^32 - 1,000 over 2,000 envs: rank 1's envs have seed + global index >= 2^32.  The
+    env seeds wrap (vec_environment.h:41, u32 parameter), the sampler seeds do not
+    (vec_sampler.h:9-13, size_t): the shards sampled with (seed, first_index=lo) equal the whole
+    batch, and the wrapped sampler base (seed + lo) & 0xffffffff -- what ranks passed before --
+    does not."""
+    n_total, seed, steps = 2000, 2 ** 32 - 1000, 40
+    merged = run_two_ranks(n_total, seed, steps)
+    full = [x.hex() for x in rollout(n_total, seed, steps)]
     assert merged == full
+    lo = n_total // 2
+    from city_of_gold.shard import shard_seed
+    wrapped = [x.hex() for x in rollout(n_total - lo, seed, steps, first=lo, sampler_seed=shard_seed(seed, lo))]
+    assert wrapped != full[lo:], "the wrapped sampler base should sample differently (the test's control)"
 
 
 def test_shard_blocks():

@@ -72,10 +72,10 @@ def test_C4_shard_n8192_hard_host_views_every_step(cg):
     lo, hi = shard(65536, 7, 8)                            # the 8th GPU's shard of C4
     n, base = hi - lo, shard_seed(12345, lo)
     env = cg.vec.get_vec_env(n)()
-    smp = cg.vec.get_vec_sampler(n)(base)
+    smp = cg.vec.get_vec_sampler(n)(12345, first_index=lo)
     env.reset(base, 4, 3, cg.HARD, 100000, False)
     runner = cg.vec.get_runner(n)(env, smp, 8)
-    orc, osm = po.OracleVec(n), po.OracleSampler(n, base)
+    orc, osm = po.OracleVec(n), po.OracleSampler(n, 12345, lo)
     orc.reset(base, 4, 3, 2, 100000)
     acts = runner.get_actions()
     sub = slice(0, n, 37)                                  # a strided subset checked every step

@@ -169,6 +169,105 @@ print("OK", int(orc.infos["total_length"].astype(bool).sum()))
 '''
 
 
+PARK_NOFIX_SCRIPT = r'''
+import sys
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import numpy as np
+import city_of_gold as cg
+import pyoracle as po
+n, j, seed, steps = int(sys.argv[3]), int(sys.argv[4]), 4242, 20
+FIELDS = ("observations", "selected_action_masks", "infos", "rewards", "dones", "agent_selection")
+
+
+def check(env, orc, keep, what):
+    for nm in FIELDS:
+        a, b = getattr(env, nm)[keep], getattr(orc, nm)[keep]
+        bad = po.named_equal(a, b) if a.dtype.names else (None if np.array_equal(a, b) else nm)
+        assert bad is None, f"{what}: {nm}.{bad} differs from the oracle"
+
+
+env = cg.vec.get_vec_env(n)(device=0)
+smp = cg.vec.get_vec_sampler(n)(seed, device=0)
+env.reset(seed, 4, 3, cg.HARD, 100000, False)
+run = cg.vec.get_runner(n)(env, smp, None, device_views=True)
+run.set_chunk(steps)
+run.rollout(steps)                        # lean_clock 0 + 20 < max_steps: launched without k_env_fixup
+try:
+    run.sync()
+    err = None
+except RuntimeError as e:
+    err = str(e)
+assert err is not None and "without its fix-up" in err, f"no F_PARK_NOFIX error: {err!r}"
+env.sync_host()
+orc, osm = po.OracleVec(n), po.OracleSampler(n, seed)
+orc.reset_threaded(seed, 4, 3, 2, 100000)
+po.run_threaded(orc, osm, steps, po.host_threads())
+others = np.ones(n, bool)
+others[j] = False
+check(env, orc, others, "the other envs after the launch")
+one, one_s = po.OracleVec(1), po.OracleSampler(1, seed, j)   # env j: a 1-env batch seeded seed + j
+one.reset(seed + j, 4, 3, 2, 100000)
+for _ in range(7):                                           # parked before its step 7
+    one_s.sample(one.selected_action_masks)
+    one.step(one_s.actions)
+for nm in FIELDS:
+    a, b = getattr(env, nm)[j:j + 1], getattr(one, nm)
+    assert (po.named_equal(a, b) if a.dtype.names else (None if np.array_equal(a, b) else nm)) is None, \
+        f"the parked env {j}: {nm} is not its state before step 7"
+del run, smp
+# the handle recovers: a reset, then launches that never reach step 7 (5-step launches).  The
+# oracles go on from their own states (a reset leaves Info alone, environment.cpp:42-77: its
+# steps_taken counts on), env j's from its 7 steps
+seed2 = 777
+smp = cg.vec.get_vec_sampler(n)(seed2, device=0)
+env.reset(seed2, 4, 3, cg.HARD, 100000, False)
+run = cg.vec.get_runner(n)(env, smp, None, device_views=True)
+run.set_chunk(5)
+run.rollout(steps)
+run.sync()
+env.sync_host()
+osm = po.OracleSampler(n, seed2)
+orc.reset_threaded(seed2, 4, 3, 2, 100000)
+po.run_threaded(orc, osm, steps, po.host_threads())
+check(env, orc, others, "after the reset")
+one_s = po.OracleSampler(1, seed2, j)
+one.reset(seed2 + j, 4, 3, 2, 100000)
+for _ in range(steps):
+    one_s.sample(one.selected_action_masks)
+    one.step(one_s.actions)
+for nm in FIELDS:
+    a, b = getattr(env, nm)[j:j + 1], getattr(one, nm)
+    assert (po.named_equal(a, b) if a.dtype.names else (None if np.array_equal(a, b) else nm)) is None, \
+        f"env {j} after the reset: {nm}"
+print("OK", err)
+'''
+
+
+@pytest.mark.parametrize("n", [4096, 40960])
+def test_trio_park_without_fixup_is_an_error(cg, tmp_path, n):
+    """The no-fix-up guard.  A trio launch that the host cleared with lean_clock (no env can park,
+    so k_env_fixup is not launched: cog_abi.cpp runner_launch_fused) must turn a park it meets
+    all the same into an error (F_PARK_NOFIX), never leave it unprocessed in silence.  The test hook
+    COG_DEBUG_PARK_NOFIX=7:j parks env j before step 7 of such a launch: runner.sync() raises
+    RuntimeError naming the missing fix-up, every other env equals the oracle after the launch,
+    env j holds its state before step 7 (a 1-env oracle seeded seed + j), and a reset of the same
+    handle runs clean afterwards.  4,096 envs (one workgroup per CU: the LAT form) and 40,960 (640
+    workgroups, two per CU)."""
+    import os
+    import subprocess
+    import sys
+    assert cg._city_of_gold.rollout_kind(n) == "trio"
+    pkg = os.path.dirname(os.path.dirname(cg.__file__))
+    oracle_dir = os.path.join(os.path.dirname(pkg), "oracle")
+    script = tmp_path / "park_nofix.py"
+    script.write_text(PARK_NOFIX_SCRIPT)
+    j = n // 2 + 37
+    r = subprocess.run([sys.executable, str(script), pkg, oracle_dir, str(n), str(j)], capture_output=True,
+                       text=True, timeout=240, env=dict(os.environ, COG_DEBUG_PARK_NOFIX=f"7:{j}"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.strip().splitlines()[-1].startswith("OK")
+
+
 @pytest.mark.parametrize("max_steps", [100000, 12])
 def test_trio_deferred_turn_end_redo_path(cg, tmp_path, max_steps):
     """The trio rollout's deferred turn end (selected masks, >= 3 players: the drawing wave runs the

@@ -99,7 +99,7 @@ dist.init_process_group("gloo")
 rank, world = dist.get_rank(), dist.get_world_size()
 lo, hi = shard(N, rank, world)
 env = cg.vec.get_vec_env(hi - lo)()                  # device from LOCAL_RANK / COG_DEVICES
-smp = cg.vec.get_vec_sampler(hi - lo)(shard_seed(SEED, lo))
+smp = cg.vec.get_vec_sampler(hi - lo)(SEED, first_index=lo)
 env.reset(shard_seed(SEED, lo), 4, 3, cg.HARD, 30, False)
 r = cg.vec.get_runner(hi - lo)(env, smp, None, device_views=True, stored_masks=True)
 r.set_chunk(50)

@@ -2,7 +2,7 @@
 
 For the N=1 headline batch (65,536 envs, 4 players, HARD, seeds 12345 + i) and for the last
 rank's shard at N = 2, 4 and 8 (`shard(65536, N-1, N)`: 32,768 / 16,384 / 8,192 envs, seeds
-`shard_seed(12345, lo)` = 12345 + global index), the engine is built by bench.py's own `make()`
+12345 + global index: `make(..., first=lo)`), the engine is built by bench.py's own `make()`
 and driven by `runner.rollout` in the two launch shapes the bench uses:
   - chunk 20: a 5-step launch (the driver's `--warmup 5`), then 20-step launches (`--steps 20`);
   - chunk 1000: 205 steps, then one 1,000-step launch (bench's default shape).
@@ -66,7 +66,7 @@ def oracle_after(world, rank):
         _oracle_cache.clear()                        # keep one shard's oracle (1.1 GB at N=1)
         lo, hi = shard(N_TOTAL, rank, world)
         n, base = hi - lo, shard_seed(SEED, lo)
-        orc, osm = po.OracleVec(n), po.OracleSampler(n, base)
+        orc, osm = po.OracleVec(n), po.OracleSampler(n, SEED, lo)
         orc.reset_threaded(base, 4, 3, 2, 100000)
         po.run_threaded(orc, osm, STEPS, po.host_threads())
         _oracle_cache[key] = (orc, osm)
@@ -91,10 +91,10 @@ def test_timed_workload_all_envs_vs_oracle(cg, world, rank, chunk):
     import torch
 
     import bench
-    from city_of_gold.shard import shard, shard_seed
+    from city_of_gold.shard import shard
     lo, hi = shard(N_TOTAL, rank, world)
-    n, base = hi - lo, shard_seed(SEED, lo)
-    env, smp, runner = bench.make(cg, n, base, 0)           # bench.py's own construction
+    n = hi - lo
+    env, smp, runner = bench.make(cg, n, SEED, 0, first=lo)   # bench.py's own construction
     runner.set_chunk(chunk)
     first = 5 if chunk == 20 else 205
     runner.rollout(first)
@@ -165,13 +165,13 @@ def test_reference_horizon_10200_steps_vs_oracle(cg, world, rank):
     lo, hi = shard(N_TOTAL, rank, world)
     n, base, steps = hi - lo, shard_seed(SEED, lo), 10200
     assert cg._city_of_gold.rollout_kind(n, 4, False) == "trio"
-    env, smp, runner = bench.make(cg, n, base, 0)
+    env, smp, runner = bench.make(cg, n, SEED, 0, first=lo)
     runner.set_chunk(1000)
     runner.rollout(steps)
     runner.sync()
     env.sync_host()
     acts = torch.from_dlpack(smp.dlpack()).cpu().numpy().view(po.ACTION).reshape(n)
-    orc, osm = po.OracleVec(n), po.OracleSampler(n, base)
+    orc, osm = po.OracleVec(n), po.OracleSampler(n, SEED, lo)
     orc.reset_threaded(base, 4, 3, 2, 100000)
     po.run_threaded(orc, osm, steps, po.host_threads())
     what = f"{n} envs (global {lo}..{hi - 1}), {steps} steps"

@@ -118,7 +118,7 @@ def test_speculative_sample_exact(cg):
             assert bad is None, f"{what} step {t}: {nm}.{bad}"
         assert np.array_equal(env.dones, orc.dones) and np.array_equal(env.agent_selection, orc.agent_selection)
 
-    ended = 0
+    ended, ended_prev, hits = 0, False, 0
     for t in range(400):
         if t == 150:                                         # another sampler steps the env once
             other.sample(masks)
@@ -128,14 +128,25 @@ def test_speculative_sample_exact(cg):
         if t == 300:                                         # a reset voids the speculation
             env.reset(seed + 1, 4, 3, cg.HARD, 25, False)
             orc.reset(seed + 1, 4, 3, 2, 25)
+        # the speculation is taken exactly when the step before was a self-publishing host step
+        # (not the first step after a reset: t = 0, 300), nothing touched the env since (t = 150,
+        # 300), no episode ended in it, and the sample reads the env's own mask view
+        expect = t not in (0, 1, 150, 300, 301) and t % 97 != 5 and not ended_prev
+        before = smp.spec_stats()
         if t % 97 == 5:                                      # a sample of a copy of the masks
             smp.sample(masks.copy())
         else:
             smp.sample(masks)
+        after = smp.spec_stats()
+        assert after[0] == before[0] + 1
+        assert after[1] - before[1] == int(expect), f"step {t}: speculative sample taken {after[1] - before[1]}, expected {int(expect)}"
+        hits += after[1] - before[1]
         osm.sample(orc.selected_action_masks)
         assert po.named_equal(acts, osm.actions) is None, f"sample at step {t}"
         env.step(acts)
         orc.step(osm.actions)
         check(t, "host loop")
+        ended_prev = bool(orc.dones.any())
         ended += int(orc.dones.sum())
     assert ended > 0, "no episode ended: the test lost a case"
+    assert hits >= 50, f"only {hits} speculative samples taken"
