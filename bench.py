@@ -425,10 +425,19 @@ def cpu_baseline(seconds):
         if best is None or rate > best[0]:
             best = (rate, threads, steps)
     rate, threads, steps = best
-    return {"value": rate, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{n} envs (the first {n} of the workload: 4p HARD seed {SEED}) x {steps} steps of "
-                      f"sample(selected masks)+step, C oracle, {threads} pinned worker threads "
-                      f"(best of thread counts {counts})"}
+    out = {"value": rate, "unit": "env-steps/s", "cores": threads, "kind": "port",
+           "sample": f"{n} envs (the first {n} of the workload: 4p HARD seed {SEED}) x {steps} steps of "
+                     f"sample(selected masks)+step, C oracle, {threads} pinned worker threads "
+                     f"(best of thread counts {counts})"}
+    try:                                               # the port's speed against the reference
+        cal = json.load(open(os.path.join(ROOT, "profiles", "calibration.json")))   # core's, same cores
+        out["port_over_reference"] = cal["port_over_reference"]
+        out["calibration"] = ("oracle/calibrate.py in the dev container (the reference cannot run on the "
+                              "GPU box): " + cal["workload"] + "; median of " + str(len(cal["ratios"])) +
+                              " interleaved reps " + ", ".join("%.2f" % x for x in cal["ratios"]))
+    except Exception:
+        pass
+    return out
 
 
 KERNEL_LABEL = {"wave": "k_env_rollout<selected>", "pipe": "k_env_rollout_pipe<selected>",

@@ -80,10 +80,19 @@ def _make_env_cls(n):
             stream = stream_handle(_C.VecEnvBase.shard_info(self, 0)[2])
         _C.VecEnvBase.step_device(self, d_actions, -1 if stream is None else int(stream))
 
+    def invalidate_device(self, stream=None):
+        """After writing device records (device_tensors / DLPack views): the next step takes them
+        as written, as the reference's views alias its live state.  Ordered after torch's current
+        stream on the env's device (or after `stream`, a hipStream_t handle; -1: no ordering)."""
+        if stream is None and self.num_shards == 1:
+            stream = stream_handle(_C.VecEnvBase.shard_info(self, 0)[2])
+        _C.VecEnvBase.invalidate_device(self, -1 if stream is None else int(stream))
+
     doc = (f"Vectorized city of gold environment for {n} environments.\n\n"
            "reset() must be called first to initialize the environments before stepping.")
     return type(VEC_ENV_CLS + str(n), (_C.VecEnvBase,), {"__init__": __init__, "__doc__": doc,
                                                          "step_device": step_device,
+                                                         "invalidate_device": invalidate_device,
                                                          "__module__": "city_of_gold.vec.sampler"})
 
 

@@ -1174,6 +1174,24 @@ int cog_env_signal_stream(cog_env *env, int k, void *stream) {
   return COG_OK;
 }
 
+int cog_env_invalidate_device(cog_env *env, void *stream) {
+  if (!env) return fail(COG_ERR_INVALID, "env is NULL");
+  int rc = prepare_host(env);
+  if (rc) return rc;
+  env_changed(env);                                        // (voids a speculative sample)
+  for (EnvShard &k : env->sh) {
+    DeviceGuard g(k.device);
+    if (stream != COG_NO_STREAM) {                         // the caller's writes: order after them
+      HIPCHK(hipEventRecord(k.ev, static_cast<hipStream_t>(stream)));
+      HIPCHK(hipStreamWaitEvent(k.stream, k.ev, 0));
+    }
+    k.lean_clock = ~0ull;                                  // (edited masks or decks: any path)
+    if (cog::launch_resync(k.s, k.stream))
+      return fail(COG_ERR_HIP, std::string("resync launch failed: ") + hipGetErrorString(hipGetLastError()));
+  }
+  return finish(env, true);                                // (the host views, when there are any)
+}
+
 int cog_env_set_autoreset(cog_env *env, int on) {
   if (!env) return fail(COG_ERR_INVALID, "env is NULL");
   int rc = sync_all(env);

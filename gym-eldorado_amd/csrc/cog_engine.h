@@ -123,7 +123,7 @@ struct DevState {
   // redo_at of each launch as if its action left the lean step (kParkRedo), so the tests exercise
   // the fix-up's redo path and the no-fix-up guard (F_PARK_NOFIX); redo_at -1 (default): off
   int32_t redo_at;
-  int64_t redo_env;
+  int32_t redo_env;
 };
 
 struct ResetParams {
@@ -139,6 +139,8 @@ int launch_init(const DevState &s, const uint32_t *seeds_host_unused, uint32_t d
                 void *stream);
 int launch_reset(const DevState &s, const ResetParams &p, void *stream);
 int launch_encode_all(const DevState &s, void *stream, int variant = 0);
+// the mask bit vectors and the Info steps mirror rebuilt from the device records (k_resync)
+int launch_resync(const DevState &s, void *stream);
 int launch_step(const DevState &s, const uint8_t *d_actions, void *stream);
 // a host-visible step whose pinned views equal the records in HBM (after a publish, no device-only
 // work since): every changed granule of a host-visible record is stored into the view and the

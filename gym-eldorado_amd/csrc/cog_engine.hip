@@ -3602,7 +3602,10 @@ DEV void cnt_store(TrioLds &D, int k, uint32_t v) {
 }
 // wait (wave-uniform) until counter `field` of c (a member of c) >= v
 DEV void cnt_wait(TrioLds &D, TrioCnt6 &c, const uint32_t &field, uint32_t v, const DevState &s) {
-  if (field >= v || c.abort) return;
+  // (the common case first, alone: one scalar compare and branch -- the sticky abort matters only
+  // to a wave that would wait)
+  if (__builtin_expect(field >= v, 1)) return;
+  if (c.abort) return;
   for (uint32_t spins = 0;; spins++) {
     cnt_read(D, c);
     if (field >= v || c.abort) return;
@@ -3846,17 +3849,23 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
       const bool fast = sample_lean(selb, pr, srng, a_play, LAT, R.tab);
       bool other = false;                                  // an action head other than play set
       if (__builtin_amdgcn_ballot_w64(!fast) && !fast) {   // (wave-uniform skip)
+#ifdef COG_ISSUE_COUNT                                     // (diagnostic ISA builds, tools/r06/issue_frac.py:
+        other = true;                                      // the rare fallback's code out of the count)
+#else
         uint8_t act[5];
         R.sel = heads_of(selb);
         step_action<SRC>(R, make_uint2(0u, 0u), srng, act);
         a_play = act[0];
         other = ((uint32_t)act[1] | act[2] | act[3] | act[4]) != 0u;
+#endif
       }
       other = other || a_play > 8u;                        // (a type >= 8: not in a narrow deck's hand)
       const bool was_done = R.done() != 0u;
       // not the lean step's case (never in the canonical loop), or the test hook: hand the env to
       // k_env_fixup before its step t
-      if (!was_done && (!lean_p || other || (t == s.redo_at && (s.redo_env < 0 || (int64_t)(wbase + i) == s.redo_env)))) {
+      bool hook = false;                                   // (test hooks: t uniform, so a scalar
+      if (t == s.redo_at) hook = s.redo_env < 0 || (int)(wbase + i) == s.redo_env;   // branch in the loop)
+      if (!was_done && (!lean_p || other || hook)) {
         srng = srng0;
         trio_store_private(s, i, R, selb);
         rngs[i] = srng;
@@ -4491,6 +4500,20 @@ __global__ void k_sync_heads(DevState s) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < s.n) sync_heads(s, i);
 }
+// cog_env_invalidate_device: after a caller wrote device records, the engine's private mirrors of
+// records the reference reads back are rebuilt from them -- the mask bit vectors from the selected
+// and stored ActionMask records (player.cpp:16-27 reads the mask bools), and the Info steps_taken
+// mirror from the Info records (environment.cpp:97: steps_taken += 1 reads the record)
+__global__ void k_resync(DevState s) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= s.n) return;
+  sync_heads(s, i);
+  const uint8_t *inf = s.info + i * COG_INFO_BYTES + COG_AGENT_INFO0;
+  uint32_t v = 0u;
+#pragma unroll
+  for (int p = 0; p < 4; p++) v |= (uint32_t)inf[COG_AGENT_INFO_STRIDE * p] << (8 * p);
+  reinterpret_cast<uint32_t *>(s.priv + i)[12] = v;        // EnvPriv::info_steps (granule 3, dword 0)
+}
 
 // Completion word of a host call: queued behind the call's work on its stream, it stores `seq`
 // into a pinned, device-mapped word that the host spins on (a system-scope release store, after
@@ -4590,6 +4613,11 @@ int launch_reset(const DevState &s, const ResetParams &p, void *stream) {
   const int epw = epw_env > 0 ? (epw_env < 64 ? epw_env : 64) : (int)(auto_epw < 1 ? 1 : auto_epw > 64 ? 64 : auto_epw);
   hipLaunchKernelGGL(k_reset, dim3(blocks_for(s.n, (unsigned)epw)), dim3(64), 0, (hipStream_t)stream, s, p, epw);
   hipLaunchKernelGGL(k_sync_heads, dim3(blocks_for(s.n, 256)), dim3(256), 0, (hipStream_t)stream, s);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int launch_resync(const DevState &s, void *stream) {
+  if (!s.n) return 0;
+  hipLaunchKernelGGL(k_resync, dim3(blocks_for(s.n, 256)), dim3(256), 0, (hipStream_t)stream, s);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int launch_encode_all(const DevState &s, void *stream, int variant) {
@@ -4771,7 +4799,7 @@ int launch_rollout(const DevState &s, int mask_source, int steps, uint32_t *d_rn
     }();
     DevState sd = s;
     sd.redo_at = park_nofix.first >= 0 ? park_nofix.first : redo_at;
-    sd.redo_env = park_nofix.first >= 0 ? (int64_t)park_nofix.second : -1;
+    sd.redo_env = park_nofix.first >= 0 ? (int32_t)park_nofix.second : -1;
     sd.park_par = (*park_seq)++ & 1u;
     // (the redo hook parks every env: never without the fix-up; $COG_ALWAYS_FIXUP for A/B)
     static const bool always_fixup = getenv("COG_ALWAYS_FIXUP") != nullptr;

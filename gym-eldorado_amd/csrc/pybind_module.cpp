@@ -451,6 +451,11 @@ PYBIND11_MODULE(_city_of_gold, m) {
       .def("signal_stream", [](VecEnv &e, uintptr_t stream, int k) {
         check(cog_env_signal_stream(e.handle(), k, reinterpret_cast<void *>(stream)));
       }, "stream"_a, "shard"_a = 0)
+      .def("invalidate_device", [](VecEnv &e, int64_t stream) {
+        // the caller wrote device records: rebuild the engine's mirrors of them (cog.h), ordered
+        // after the work queued on `stream` (-1: no ordering)
+        check(cog_env_invalidate_device(e.handle(), stream < 0 ? COG_NO_STREAM : reinterpret_cast<void *>((uintptr_t)stream)));
+      }, "stream"_a = -1)
       .def("set_autoreset", [](VecEnv &e, bool on) { check(cog_env_set_autoreset(e.handle(), on ? 1 : 0)); }, "on"_a)
       .def("stream", [](VecEnv &e, int k) { return (uintptr_t)cog_env_shard_stream(e.handle(), k); }, "shard"_a = 0)
       .def("hazards", [](VecEnv &e) {

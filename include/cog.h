@@ -148,6 +148,14 @@ COG_API void *cog_env_shard_stream(cog_env *env, int shard);
  * signal_stream: work queued later on `stream` runs after the engine work queued on shard k */
 COG_API int cog_env_wait_stream(cog_env *env, int shard, void *stream);
 COG_API int cog_env_signal_stream(cog_env *env, int shard, void *stream);
+/* after the caller wrote the env's device records (DLPack views / d_* pointers), ordered after
+ * the work queued on `stream` so far (COG_NO_STREAM: none): the engine takes the records as they
+ * now are, as the reference's views alias its live state (include/pybind/common.h:97-101) -- the
+ * decks, phase, resources and shop are read from the records anyway; the selected and stored
+ * ActionMask records (0/1 bytes) and Info steps_taken also feed the engine's private mirrors, which
+ * this rebuilds.  Host views are refreshed when the env has them.  Without this call, writes to
+ * those records are not seen by the next step (see INTEGRATION.md "Device views"). */
+COG_API int cog_env_invalidate_device(cog_env *env, void *stream);
 /* diagnostics: re-run the map-observation encode (map.cpp:389-405) over all envs `iters`
  * times back to back; average device time per launch (HIP events).  Output is unchanged.
  * variant: 0 = production kernel, >0 = alternative implementations kept for A/B timing. */

@@ -32,7 +32,6 @@ L.cog_last_error.restype = C.c_char_p
 vp = C.c_void_p
 L.cog_env_create.argtypes = [C.c_size_t, C.c_int, C.POINTER(vp)]
 L.cog_env_reset.argtypes = [vp, C.c_uint32, C.c_uint8, C.c_uint8, C.c_int, C.c_uint32, C.c_int]
-L.cog_env_sync_host.argtypes = [vp]
 L.cog_sampler_create.argtypes = [C.c_size_t, C.c_uint64, C.c_int, C.POINTER(vp)]
 L.cog_sampler_actions.restype = vp
 L.cog_sampler_actions.argtypes = [vp]
@@ -67,13 +66,12 @@ env, smp, run = vp(), vp(), vp()
 ok(L.cog_env_create(n, 0, C.byref(env)))
 ok(L.cog_env_reset(env, seed, 4, 3, 2, max_steps, 0))
 ok(L.cog_sampler_create(n, seed, 0, C.byref(smp)))
-ok(L.cog_runner_create(env, smp, 0, 1, C.byref(run)))       # COG_RUNNER_DEVICE_VIEWS
+v = Views()
+ok(L.cog_env_get_views(env, C.byref(v)))                     # host views: sync() refreshes them
+ok(L.cog_runner_create(env, smp, 0, 0, C.byref(run)))        # (and the sampler's actions view)
 ok(L.cog_runner_set_chunk(run, 20))
 ok(L.cog_runner_rollout(run, steps))
 ok(L.cog_runner_sync(run))
-v = Views()
-ok(L.cog_env_get_views(env, C.byref(v)))
-ok(L.cog_env_sync_host(env))
 orc, osm = po.OracleVec(n), po.OracleSampler(n, seed)
 orc.reset_threaded(seed, 4, 3, 2, max_steps)
 po.run_threaded(orc, osm, steps, po.host_threads())

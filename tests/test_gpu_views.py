@@ -150,3 +150,55 @@ def test_speculative_sample_exact(cg):
         ended += int(orc.dones.sum())
     assert ended > 0, "no episode ended: the test lost a case"
     assert hits >= 50, f"only {hits} speculative samples taken"
+
+
+def test_device_record_writes_taken_after_invalidate(cg):
+    """Writes into the device records (DLPack views) are taken by the next step after
+    env.invalidate_device(), as the reference's views alias its live state
+    (include/pybind/common.h:97-101): the selected ActionMask is the deck's live mask
+    (player.cpp:16-27, environment.cpp:31-37), a player's stored mask is what its next turn loads
+    (environment.cpp:62-63), the decks are the Deck's piles, and Info steps_taken counts on from
+    the record (environment.cpp:97).  The oracle is fed the same bytes; then 40 more steps through
+    the runner's device loop (the trio) must equal it everywhere."""
+    import torch
+    n, seed = 256, 9090
+    env, smp, orc, osm = make(cg, n, seed)
+    run = cg.vec.get_runner(n)(env, smp, None, device_views=True)
+    run.set_chunk(20)
+    run.rollout(40)
+    run.sync()
+    po.run_threaded(orc, osm, 40, po.host_threads())
+    t = cg.device_tensors(env)
+    sel, obs, info = t["selected_action_masks"], t["observations"], t["infos"]
+    ag = orc.agent_selection.copy()
+    edits = []                                               # (tensor name, env, byte offset, value)
+    for i in range(32):                                      # the selected mask: pass only
+        edits += [("sel", i, 0, 1)] + [("sel", i, b, 0) for b in range(1, 22)]
+    p40 = (int(ag[40]) + 1) % 4                              # a deck: one more Explorer in the discard
+    off40 = 16192 + 256 * p40 + 84
+    edits.append(("obs", 40, off40, int(orc.observations.view(np.uint8).reshape(n, -1)[40, off40]) + 1))
+    p50 = (int(ag[50]) + 1) % 4                              # the next player's stored mask: pass only
+    for b in range(22):
+        edits.append(("obs", 50, 16192 + 256 * p50 + 128 + b, 1 if b == 0 else 0))
+    edits.append(("info", 7, 4 + 32 * int(ag[7]), 200))     # Info steps_taken of the acting player
+    host = {"sel": orc.selected_action_masks.view(np.uint8).reshape(n, -1),
+            "obs": orc.observations.view(np.uint8).reshape(n, -1),
+            "info": orc.infos.view(np.uint8).reshape(n, -1)}
+    dev = {"sel": sel, "obs": obs, "info": info}
+    for nm, i, off, v in edits:
+        dev[nm][i, off] = v                                  # (on torch's current stream)
+        host[nm][i, off] = v
+    env.invalidate_device()                                  # (ordered after those writes)
+    run.rollout(40)
+    run.sync()
+    env.sync_host()
+    po.run_threaded(orc, osm, 40, po.host_threads())
+    for nm in ("observations", "selected_action_masks", "infos"):
+        bad = po.named_equal(getattr(env, nm), getattr(orc, nm))
+        assert bad is None, f"{nm}.{bad} differs from the oracle fed the same edits"
+    for nm in ("rewards", "dones", "agent_selection"):
+        assert np.array_equal(getattr(env, nm), getattr(orc, nm)), nm
+    acts = torch.from_dlpack(smp.dlpack()).cpu().numpy().view(po.ACTION).reshape(n)
+    assert po.named_equal(acts, osm.actions) is None
+    # the edits mattered: pass-only envs passed, env 7 counted on from 200
+    assert int(orc.infos["agent_infos"]["steps_taken"][7].max()) >= 200

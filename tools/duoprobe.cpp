@@ -109,6 +109,32 @@ int main(int argc, char **argv) {
       if (wpg == 4) {                                      // the launch timeline (stepping waves, 100 MHz)
         unsigned long long t0 = ~0ull;
         for (size_t w = 0; w < waves; w += wpg) t0 = std::min(t0, h[w * K + 10]);
+        // per round of blocks ($PROBE_ROUND blocks each, default 512 = two workgroups per CU): the
+        // hardware's rounds of workgroups, or a multi-block launch's k-th block of each workgroup
+        const size_t rb = getenv("PROBE_ROUND") ? strtoul(getenv("PROBE_ROUND"), nullptr, 10) : 512;
+        const size_t nblk = waves / wpg;
+        for (size_t r0 = 0; nblk > rb && r0 < nblk; r0 += rb) {
+          printf("  round of blocks %zu..%zu (us after the first stepper start; median / max):\n", r0,
+                 std::min(nblk, r0 + rb) - 1);
+          const char *nm[6] = {"block start", "prologue done", "last step done", "other waves done (FIN)",
+                               "epilogue stores issued", "prologue loads done"};
+          for (int k = 10; k < 16; k++) {
+            std::vector<double> v;
+            for (size_t b = r0; b < std::min(nblk, r0 + rb); b++) v.push_back((double)(h[b * wpg * K + k] - t0) * 0.01);
+            printf("    stepping   %-31s %8.2f %8.2f\n", nm[k - 10], med(v), *std::max_element(v.begin(), v.end()));
+          }
+          const char *rn2[4] = {"stepping", "drawing", "storing A", "storing B"};
+          for (int role = 1; role < 4; role++) {
+            const int ks[4] = {14, 15, 11, 12};
+            const char *kn[4] = {"block start", "prologue done", "last record's wait returned", "loop done"};
+            for (int j = 0; j < 4; j++) {
+              std::vector<double> v;
+              for (size_t b = r0; b < std::min(nblk, r0 + rb); b++)
+                v.push_back((double)(h[(b * wpg + role) * K + ks[j]] - t0) * 0.01);
+              printf("    %-10s %-31s %8.2f %8.2f\n", rn2[role], kn[j], med(v), *std::max_element(v.begin(), v.end()));
+            }
+          }
+        }
         const char *tl_names[5] = {"stepper start (after the table barrier)", "prologue done (barrier B)",
                                    "last step done", "other waves done (FIN)", "epilogue stores issued"};
         printf("  launch timeline of a %d-step launch (us after the first stepper start; median / max over workgroups):\n", chunk);
