@@ -61,6 +61,7 @@ WRITEBACK_BYTES = 1234      # D2H / write-back bytes per env-step (C4
 ENCODE_BYTES = 18432        # per encoded env (16,128 written + 2,304 read)
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 N_SIMD, CLOCK_HZ, VALU_CYC = 1024, 2.4e9, 2.0   # 256 CUs x 4 SIMD-32; wave64 VALU = 2 cycles
+N_CU = 256                  # the trio's one-workgroup-per-CU (LAT) form up to N_CU workgroups of 64 envs
 METRIC = "env-steps/sec at n_envs=65536, 4 players; bit-exact vs C++ ref"
 HAZ_ERASE_PAST = 0x02       # map.cpp:727 erase past the end: GCC>=13 libstdc++ semantics (oracle-pinned)
 
@@ -445,7 +446,7 @@ KERNEL_LABEL = {"wave": "k_env_rollout<selected>", "pipe": "k_env_rollout_pipe<s
                 "trio": "k_env_rollout_trio<selected> + k_env_fixup<selected>"}
 
 
-def roofline(prof, n, k_chunk, launch_s, kind="trio", stamps=None):
+def roofline(prof, n, k_chunk, launch_s, kind="trio", stamps=None, issue=None):
     """The dominant kernel -- the persistent rollout that runs a shard of n envs (`kind`: trio, wave,
     pipe or duo, cog_rollout_kind) -- against HBM, by the bytes it really moves: `traffic` is the HBM
     bytes of one launch of this exact engine source AT THIS LAUNCH SHAPE (n envs, k steps per launch,
@@ -506,6 +507,22 @@ def roofline(prof, n, k_chunk, launch_s, kind="trio", stamps=None):
         out["limiter"].update({k: st[k] for k in ("busy_ticks_per_step", "wait_ticks_per_step", "ticks_per_step",
                                                   "busy_frac", "steps_per_launch") if k in st})
         out["limiter"]["source"] = "profiles/stamps_profile.json (tools/duoprobe.cpp -DCOG_STAMPS, same engine source)"
+    form = "lat" if (n + 63) // 64 <= N_CU else "two_per_cu"     # (cog_engine.hip launch_rollout's trio_jt)
+    ip = (issue or {}).get(form)
+    if st and ip and ip.get("ticks_per_step_issue") and kind == "trio":
+        busy = st["busy_ticks_per_step"]
+        out["limiter"]["issue_frac"] = ip["ticks_per_step_issue"] / busy
+        out["limiter"]["dependent_chain_frac"] = ip["ticks_per_step_dependent"] / busy
+        out["limiter"]["issue"] = {
+            "per_step_instructions": ip["per_step_instructions"], "mix": ip["mix"], "kernel_form": form,
+            "issue_ticks_per_step": ip["ticks_per_step_issue"], "dependent_ticks_per_step": ip["ticks_per_step_dependent"],
+            "busy_ticks_per_step": busy,
+            "note": "issue_frac = the stepping wave's per-step instructions (static count of its step loop without the "
+                    "spin waits or the never-taken sampling fallback: an upper bound of what it issues) x a lone "
+                    "wave's cost per instruction of each kind when it has independent work (tools/r06/chainprobe.hip) "
+                    "/ its measured busy ticks per step: near 1 = issue-bound, the chain at its floor; "
+                    "dependent_chain_frac: the same with every instruction waiting for the one before "
+                    "(profiles/issue_profile.json, tools/r06/issue_frac.py, same engine source)"}
     pw = (e or {}).get("per_wave_step") or {}
     if pw.get("valu"):
         achieved = pw["valu"] * waves * k_chunk / launch_s
@@ -519,12 +536,13 @@ def roofline(prof, n, k_chunk, launch_s, kind="trio", stamps=None):
     return out
 
 
-def load_stamps():
-    """profiles/stamps_profile.json when it was measured on this exact engine source; else None."""
+def load_stamps(name="stamps_profile.json"):
+    """profiles/<name> (stamps_profile.json, issue_profile.json) when it was measured on this exact
+    engine source; else None."""
     try:
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         from pmc_profile import engine_hash
-        with open(os.path.join(ROOT, "profiles", "stamps_profile.json")) as f:
+        with open(os.path.join(ROOT, "profiles", name)) as f:
             p = json.load(f)
         return p if p.get("engine_sha") == engine_hash() else None
     except Exception:
@@ -582,7 +600,8 @@ def main():
     k_chunk = min(chunk, args.steps)
     launch_s = kernel_time(runner, k_chunk, max(3, min(20, 4000 // max(k_chunk, 1))))
     prof = load_profile()
-    roof = roofline(prof, n, k_chunk, launch_s, cg._city_of_gold.rollout_kind(n, N_PLAYERS, False), load_stamps())
+    roof = roofline(prof, n, k_chunk, launch_s, cg._city_of_gold.rollout_kind(n, N_PLAYERS, False), load_stamps(),
+                    load_stamps("issue_profile.json"))
 
     haz, per = env.hazards()
     n_erase = int(((per & HAZ_ERASE_PAST) != 0).sum())

@@ -149,6 +149,14 @@ def test_bench_roofline_store_model():
     assert abs(r["store_model"]["frac"] - t_store / launch) < 1e-12
     assert abs(r["env_steps_per_s"] - n * k / launch) < 1e-6 * r["env_steps_per_s"]
     assert r["valu_issue"]["valu_per_wave_step"] == 1000.0 and r["kernel"].startswith("k_env_rollout_trio")
+    issue = {"two_per_cu": {"per_step_instructions": 600, "mix": {"valu": 200, "salu": 400},
+                            "ticks_per_step_issue": 1800.0, "ticks_per_step_dependent": 5400.0},
+             "lat": {"per_step_instructions": 500, "mix": {"valu": 100, "salu": 400},
+                     "ticks_per_step_issue": 900.0, "ticks_per_step_dependent": 4000.0}}
+    ri = bench.roofline(prof, n, k, launch, "trio", stamps, issue)     # 65,536 envs: two per CU
+    assert ri["limiter"]["issue_frac"] == 1800.0 / 3000.0 and ri["limiter"]["dependent_chain_frac"] == 5400.0 / 3000.0
+    assert ri["limiter"]["issue"]["kernel_form"] == "two_per_cu"
+    assert "issue_frac" not in r["limiter"]                          # (no issue profile given)
     small = bench.roofline(prof, 8192, k, 50e-6, "duo")            # its own entry, not the 65,536 one
     assert small["traffic"] == 2.1e7 and small["kernel"].startswith("k_env_rollout_duo")
     assert "busy_frac" not in small["limiter"]

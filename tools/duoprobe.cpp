@@ -92,7 +92,7 @@ int main(int argc, char **argv) {
                                          "prologue (per launch)", "drain (per launch)", "epilogue (per launch)", "wait: ring slot",
                                          "", "", "", "", "", ""};
       const char *role_name[4] = {"stepping", wpg == 4 ? "drawing" : "storing", "storing A", "storing B"};
-      if (getenv("PROBE_JSON") && wpg == 4) {              // one line for tools/r05/stamps_profile.py
+      if (getenv("PROBE_JSON") && wpg == 4) {              // one line for tools/stamps_profile.py
         double ph[16];
         for (int k = 0; k < 16; k++) {
           std::vector<double> v;

@@ -1,11 +1,11 @@
 """Diagnostic: steady full dynamics (stored masks, max_steps 100,000) at 65,536 envs with each
 rollout kernel ($COG_ROLLOUT is read once per process: one kernel per run).
-    COG_ROLLOUT=wave|pipe|duo python tools/r05/fd_kinds.py [envs]"""
+    COG_ROLLOUT=wave|pipe|duo python tools/fd_kinds.py [envs]"""
 import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gym-eldorado_amd"))
 import city_of_gold as cg  # noqa: E402
 

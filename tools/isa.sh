@@ -1,6 +1,6 @@
 #!/bin/bash
 # Disassembly of one kernel of the built engine object (no GPU needed).
-#     tools/r05/isa.sh [kernel symbol substring] > out.s
+#     tools/isa.sh [kernel symbol substring] > out.s
 set -e
 B=/opt/rocm/lib/llvm/bin
 O=${OBJ:-gym-eldorado_amd/build/cog_engine.hip.o}

@@ -1,19 +1,20 @@
 """The stepping wave's per-step instruction count from the trio kernel's ISA (diagnostic; no GPU).
 
-    python tools/r06/issue_frac.py [--obj OBJ] [--lat 0|1] [--json profiles/issue_profile.json]
+    python tools/issue_frac.py [--obj OBJ] [--lat 0|1] [--chain profiles/r06_chainprobe.txt]
+                                   [--json profiles/issue_profile.json]
 
 Compiles the engine with -DCOG_ISSUE_COUNT (the product source with the stepping wave's rare
 sampling fallback -- step_action behind the wave-uniform `ballot(!fast)` skip, never taken on a
 canonical step -- replaced by a park, so that its code is out of the listing; build/ is left
 alone, the object goes to /tmp unless --obj names one), disassembles k_env_rollout_trio
-(tools/r05/isa.sh), takes the stepping wave's region (from its s_setprio 3 to the kernel's end)
+(tools/isa.sh), takes the stepping wave's region (from its s_setprio 3 to the kernel's end)
 and in it the step loop: the largest loop whose body holds the ring record's ds_write_b128
 stores and no s_barrier (the per-block prologue's).  The count leaves out the progress waits'
 spin loops (s_sleep); what remains is an upper bound of what a wave issues on a canonical step:
 every lane-divergent `if` of the lean step is issued whenever any of the 64 lanes takes it, which
 in a 64-env wave is nearly every step, and the park paths (skipped when no lane parks) are
 counted too.  bench.py's roofline.limiter.issue_frac =
-this count x the lone-wave dependent-chain cost per instruction (tools/r06/chainprobe.hip,
+this count x the lone-wave dependent-chain cost per instruction (tools/chainprobe.hip,
 profiles/*_chainprobe.txt) / the stepping wave's measured busy ticks per step
 (profiles/stamps_profile.json).
 """
@@ -25,13 +26,13 @@ import re
 import subprocess
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def disasm(obj, lat):
     sym = "k_env_rollout_trioILi0ELb%d" % lat
     env = dict(os.environ, OBJ=obj)
-    return subprocess.run(["bash", os.path.join(ROOT, "tools/r05/isa.sh"), sym], capture_output=True, text=True,
+    return subprocess.run(["bash", os.path.join(ROOT, "tools/isa.sh"), sym], capture_output=True, text=True,
                           env=env, check=True).stdout
 
 
@@ -90,6 +91,7 @@ def main():
     ap.add_argument("--obj")
     ap.add_argument("--lat", type=int, default=None)
     ap.add_argument("--json")
+    ap.add_argument("--chain")
     a = ap.parse_args()
     if not a.obj:                                          # the COG_ISSUE_COUNT build of this source
         sys.path.insert(0, os.path.join(ROOT, "gym-eldorado_amd"))
@@ -100,6 +102,23 @@ def main():
     res = {}
     for lat in ([a.lat] if a.lat is not None else [0, 1]):
         res["lat" if lat else "two_per_cu"] = count(parse(disasm(a.obj, lat)), lat)
+    if a.chain:                                            # the lone-wave costs (tools/chainprobe.hip)
+        cost = {}
+        for line in open(a.chain):
+            m = re.match(r"CHAIN (.+?)\s+([\d.]+) ticks per link,\s+([\d.]+) per instruction \(lone wave, (\w+)\)", line)
+            if m:
+                cost[m.group(1).strip()] = float(m.group(3))
+        res["costs"] = {
+            "issue": {"valu": cost["ISSUE 4 x v_add_u32"], "salu": cost["ISSUE 4 x s_add_u32"],
+                      "lds": cost["ISSUE 4 x ds_read_b32 + wait"], "vmem": cost["ISSUE 4 x ds_read_b32 + wait"]},
+            "dependent": {"valu": cost["v_add_u32"], "salu": cost["s_add_u32"],
+                          "lds": cost["ds_read_b32+wait+v_and"], "vmem": cost["ds_read_b32+wait+v_and"]},
+            "source": os.path.relpath(a.chain, ROOT), "unit": "s_memtime ticks per instruction (the stamps' unit)"}
+        for key in ("lat", "two_per_cu"):
+            if key in res:
+                mix = res[key]["mix"]
+                for form in ("issue", "dependent"):
+                    res[key]["ticks_per_step_" + form] = sum(mix.get(t, 0) * res["costs"][form][t] for t in mix)
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     try:
         from pmc_profile import engine_hash

@@ -1,6 +1,6 @@
 """Static instruction count of the outermost loop of a wave's region in an llvm-objdump listing
-(diagnostic: tools/r05/isa.sh output).  Spin loops (those containing s_sleep) are excluded.
-    python tools/r05/loopcount.py listing.s FIRST_LINE LAST_LINE"""
+(diagnostic: tools/isa.sh output).  Spin loops (those containing s_sleep) are excluded.
+    python tools/loopcount.py listing.s FIRST_LINE LAST_LINE"""
 import collections
 import re
 import sys

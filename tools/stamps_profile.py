@@ -3,13 +3,13 @@ the trio stepping wave's s_memtime ticks per step, split into its own work (busy
 the other waves' progress counters, per shard size, stamped with the engine source hash so that
 bench.py attaches it (roofline.limiter) only to the engine it measured.
 
-    python tools/r05/stamps_profile.py <duoprobe output file> [...] > profiles/stamps_profile.json
+    python tools/stamps_profile.py <duoprobe output file> [...] > profiles/stamps_profile.json
 """
 import json
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 from pmc_profile import engine_hash  # noqa: E402
 
