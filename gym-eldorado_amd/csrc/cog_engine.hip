@@ -3601,6 +3601,13 @@ DEV void cnt_store(TrioLds &D, int k, uint32_t v) {
 #endif
 }
 // wait (wave-uniform) until counter `field` of c (a member of c) >= v
+#ifdef COG_ISSUE_COUNT
+// (diagnostic ISA builds, tools/issue_frac.py: the no-wait path alone -- what a step issues when
+// the counter it needs is already there; the waits are the stamps' own phases)
+DEV void cnt_wait(TrioLds &, TrioCnt6 &, const uint32_t &field, uint32_t v, const DevState &) {
+  if (field < v) asm volatile("s_nop 0");
+}
+#else
 DEV void cnt_wait(TrioLds &D, TrioCnt6 &c, const uint32_t &field, uint32_t v, const DevState &s) {
   // (the common case first, alone: one scalar compare and branch -- the sticky abort matters only
   // to a wave that would wait)
@@ -3622,6 +3629,7 @@ DEV void cnt_wait(TrioLds &D, TrioCnt6 &c, const uint32_t &field, uint32_t v, co
     __builtin_amdgcn_s_sleep(2);                           // (1 or 0: the same, r05y2)
   }
 }
+#endif
 // the stepping wave's presampled record: {the state the step starts from, head 0's index for every
 // play-head size k = 2..9 (4 bits each: uid_tab_accepted of the first draw, the narrow hand's play
 // head holds at most the pass bit and types 0-7), the state after the five draws | any draw could be
@@ -3843,13 +3851,30 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     PH(2);
     bool ended = false, finish = false, turn_end = false, stepped = false;
     uint32_t a_play = 0u;
-    if (live) {
+    // (round 6: the common path computed by every lane with selects -- no exec-mask branches, which
+    // a 64-env wave would take on nearly every step anyway; the rare parts keep their branches)
+    {
       const uint32_t srng0 = srng;
-      const uint3 pr = have_next ? pr_next : D.pre[t & (kTrioLead - 1)][l];
-      const bool fast = sample_lean(selb, pr, srng, a_play, LAT, R.tab);
+      uint3 pr = pr_next;                                  // (have_next is wave-uniform: a scalar
+      if (!have_next) pr = D.pre[t & (kTrioLead - 1)][l];  // branch, not a select of addresses)
+      // head 0's draw from the presampled record when the state is the one it starts from and heads
+      // 1-4 are {0} (then the five draws are the presampled ones: act 1-4 = 0; sample_lean)
+      const uint32_t m0 = selb.w0 & 0x3fffffu, k0 = __popc(m0);
+      const bool fast = live && pr.x == srng && (pr.z >> 31) == 0u && heads14_zero(selb) && k0 - 1u < 9u;
+      uint32_t j;
+      if (LAT) {
+        j = (pr.y >> (4u * ((k0 - 2u) & 7u))) & 15u;      // (head 0's index table, k0 = 2..9)
+      } else {
+        const UidEntry e0 = R.tab[k0 & (kUidTab - 1)];
+        j = uid_tab_accepted(pr.y, e0.s, e0.m);
+      }
+      j = fast && k0 >= 2u ? j : 0u;
+      const uint32_t a0 = nth_set_bit_iter(m0, j);
+      a_play = fast ? a0 : 0u;
+      srng = fast ? pr.z : srng;
       bool other = false;                                  // an action head other than play set
-      if (__builtin_amdgcn_ballot_w64(!fast) && !fast) {   // (wave-uniform skip)
-#ifdef COG_ISSUE_COUNT                                     // (diagnostic ISA builds, tools/r06/issue_frac.py:
+      if (__builtin_amdgcn_ballot_w64(live && !fast) && live && !fast) {   // (wave-uniform skip)
+#ifdef COG_ISSUE_COUNT                                     // (diagnostic ISA builds, tools/issue_frac.py:
         other = true;                                      // the rare fallback's code out of the count)
 #else
         uint8_t act[5];
@@ -3861,56 +3886,64 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
       }
       other = other || a_play > 8u;                        // (a type >= 8: not in a narrow deck's hand)
       const bool was_done = R.done() != 0u;
-      // not the lean step's case (never in the canonical loop), or the test hook: hand the env to
+      // not the lean step's case (never in the canonical loop), or the test hooks: hand the env to
       // k_env_fixup before its step t
       bool hook = false;                                   // (test hooks: t uniform, so a scalar
       if (t == s.redo_at) hook = s.redo_env < 0 || (int)(wbase + i) == s.redo_env;   // branch in the loop)
-      if (!was_done && (!lean_p || other || hook)) {
+      const bool parks = live && !was_done && (!lean_p || other || hook);
+      stepped = live && !was_done && !parks;               // cog_env::step, the lean case (Info steps
+      if (__builtin_amdgcn_ballot_w64(parks) && parks) {   // and the resources: the drawing wave's)
         srng = srng0;
+#ifndef COG_ISSUE_COUNT                                    // (a rare lane's stores: out of the count)
         trio_store_private(s, i, R, selb);
         rngs[i] = srng;
+#endif
         if (!lat) D.pl[ag][l] = pack_lean_player(pp, n_in_hand, n_active, steps_taken);   // (the epilogue's)
         park = (uint32_t)t | kParkRedo;
         live = false;
-      } else if (!was_done) {                              // cog_env::step, the lean case
-        stepped = true;                                    // (Info steps and the resources: the
-        uint32_t phase = R.sh[0] & 0xffu;                  // drawing wave's)
-        if (phase == COG_PHASE_INACTIVE) phase = COG_PHASE_MOVEMENT;
-        if (!lat) steps_taken = (steps_taken + 1u) & 0xffu;
-        if (a_play) {                                      // Player::play_card (player.cpp:45-60)
-          const int c = (int)a_play - 1;
-          const uint32_t prev = hand_take(H, c);           // Deck::activate's hand part (the active
-                                                           // pile and the counters: the drawing wave)
-          // the play bit (its special bit stays clear: types 0-7 are not special, is_special; a
-          // type >= 8 has parked above)
-          const uint32_t bp = 1u << (c + 1);
-          selb.w0 = prev > 1u ? (selb.w0 | bp) : (selb.w0 & ~bp);
-          if (!lat) {
-            n_in_hand = (n_in_hand - 1u) & 0xffu;
-            n_active = (n_active + 1u) & 0xffu;
-            pp.z = (pp.z & ~0xffu) | (uint32_t)c;          // idx_last
-          }
-        } else {
-          phase = phase == COG_PHASE_BUYING ? COG_PHASE_INACTIVE : phase + 1u;   // pass: next phase
-        }
-        turn_end = phase == COG_PHASE_INACTIVE;            // maybe_end_turn -> next_agent
-        if (turn_end) {                                    // (Player::end_turn: the drawing wave)
-          n_active = 0u;
-          stab = selb;                                     // save_actionmask
-          R.set_agent((uint32_t)na);
-          selb = stnb;                                     // load_actionmask (na != ag: >= 3 players)
-          stnb.w2 = (stnb.w2 & ~kMoveShopBits) | 0x204u;   // update_observation, INACTIVE phase
-          R.turn_counter++;
-        }
-        R.sh[0] = (R.sh[0] & ~0xffu) | phase;
-        // done (environment.cpp:183-207): the (next) agent's cell or the turn counter.  Both change
-        // only with the turn here (no move: the agent's cell is the one checked after its last
-        // step, never an end; a player's own cell is never an out-of-bounds lookup)
-        finish = turn_end && (COG_HEX_END((own >> (8 * na)) & 0xffu) || R.turn_counter >= R.max_steps);
-        if (finish) R.set_done(1u);
-        PH(0);
       }
-      ended = was_done || finish;
+      uint32_t phase = R.sh[0] & 0xffu;
+      if (phase == COG_PHASE_INACTIVE) phase = COG_PHASE_MOVEMENT;
+      if (!lat) steps_taken = stepped ? (steps_taken + 1u) & 0xffu : steps_taken;
+      // Player::play_card (player.cpp:45-60): Deck::activate's hand part (the active pile and the
+      // counters: the drawing wave); the play bit (its special bit stays clear: types 0-7 are not
+      // special, is_special; a type >= 8 has parked above)
+      const bool play = stepped && a_play != 0u;
+      const int c = (int)((a_play - 1u) & 7u);
+      uint2 Hp = H;
+      const uint32_t prev = hand_take(Hp, c);
+      H = play ? Hp : H;
+      const uint32_t bp = 1u << (c + 1);
+      selb.w0 = play ? (prev > 1u ? (selb.w0 | bp) : (selb.w0 & ~bp)) : selb.w0;
+      if (!lat) {
+        n_in_hand = play ? (n_in_hand - 1u) & 0xffu : n_in_hand;
+        n_active = play ? (n_active + 1u) & 0xffu : n_active;
+        pp.z = play ? (pp.z & ~0xffu) | (uint32_t)c : pp.z;   // idx_last
+      }
+      const uint32_t nph = phase == COG_PHASE_BUYING ? COG_PHASE_INACTIVE : phase + 1u;   // pass: next phase
+      phase = stepped && !play ? nph : phase;
+      turn_end = stepped && phase == COG_PHASE_INACTIVE;   // maybe_end_turn -> next_agent
+      // (Player::end_turn: the drawing wave) save_actionmask, load_actionmask (na != ag: >= 3
+      // players), update_observation's INACTIVE phase for the next player's stored mask
+      n_active = turn_end ? 0u : n_active;
+      const MBits sel0 = selb;
+      selb.w0 = turn_end ? stnb.w0 : selb.w0;
+      selb.w1 = turn_end ? stnb.w1 : selb.w1;
+      selb.w2 = turn_end ? stnb.w2 : selb.w2;
+      stab.w0 = turn_end ? sel0.w0 : stab.w0;
+      stab.w1 = turn_end ? sel0.w1 : stab.w1;
+      stab.w2 = turn_end ? sel0.w2 : stab.w2;
+      stnb.w2 = turn_end ? (stnb.w2 & ~kMoveShopBits) | 0x204u : stnb.w2;
+      R.g1y = turn_end ? (R.g1y & ~0xffu) | ((uint32_t)na & 0xffu) : R.g1y;   // R.set_agent(na)
+      R.turn_counter += turn_end ? 1u : 0u;
+      R.sh[0] = stepped ? (R.sh[0] & ~0xffu) | phase : R.sh[0];
+      // done (environment.cpp:183-207): the (next) agent's cell or the turn counter.  Both change
+      // only with the turn here (no move: the agent's cell is the one checked after its last step,
+      // never an end; a player's own cell is never an out-of-bounds lookup)
+      finish = turn_end && (COG_HEX_END((own >> (8 * na)) & 0xffu) || R.turn_counter >= R.max_steps);
+      R.g1x = finish ? (R.g1x & 0x00ffffffu) | (1u << 24) : R.g1x;   // R.set_done(1)
+      PH(0);
+      ended = live && (was_done || finish);
     }
     uint4(*ring)[64] = D.ring[sl];
     int ag1 = ag, na1 = na;
@@ -3923,27 +3956,28 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     // drawing wave is past their last turn ends; read ahead of the record's stores, so that their
     // latency overlaps them
     // (read ahead at an earlier step of the turn when the drawing wave was past them: pf_ok)
-    uint2 hd = pf_hd;
-    uint4 pla = pf_pla, hdn = pf_hdn;
+    // (the records land in pf_* themselves: the turn change below takes them from there, and
+    // re-reads ahead after it -- no copies of ten dwords through every step)
     const bool slow = tc && !pf_ok;
     if (__builtin_amdgcn_ballot_w64(slow)) {
       const int need = R.n_players() == 3u ? te1 : te2;   // the later of ag1's and na1's last turn ends
       // the drawing wave past record max(need) over the wave: its distance from t by ballots (no
       // cross-lane shuffles, which go through LDS); >= 2 in play (>= 3 players, turns of >= 2
-      // steps), and from 5 on it asks for a little more than it needs
-      const bool w = slow && need >= 0;
-      if (__builtin_amdgcn_ballot_w64(w)) {
+      // steps), and from 5 on it asks for a little more than it needs.  (needw folds the lane's
+      // condition into the value, so that each ballot is one compare)
+      const int needw = slow && need >= 0 ? need : INT32_MIN;
+      if (__builtin_amdgcn_ballot_w64(needw >= 0)) {
         int dmin = 5;
 #pragma unroll
-        for (int d = 4; d >= 1; d--) dmin = __builtin_amdgcn_ballot_w64(w && need >= t - d) ? d : dmin;
+        for (int d = 4; d >= 1; d--) dmin = __builtin_amdgcn_ballot_w64(needw >= t - d) ? d : dmin;
         PH(4);
         cnt_wait(D, cc, cc.draw, (uint32_t)(t - dmin + 1), s_glob);
         PH(5);
       }
       if (slow) {
-        hd = D.img[ag1][1][l];
-        pla = D.pl[ag1][l];
-        hdn = D.heads[na1][l];
+        pf_hd = D.img[ag1][1][l];
+        pf_pla = D.pl[ag1][l];
+        pf_hdn = D.heads[na1][l];
       }
     }
     if (live) {
@@ -3965,14 +3999,14 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
     if (tc) {
       te2 = te1;
       te1 = t;
-      H = hd;                                              // its hand from the drawing wave
-      pp = pla;
-      n_in_hand = (pla.y >> 8) & 0xffu;
-      n_active = (pla.y >> 16) & 0xffu;
-      steps_taken = (pla.z >> 8) & 0xffu;
-      lean_p = narrow && lean_player(pla);
+      H = pf_hd;                                           // its hand from the drawing wave
+      pp = pf_pla;
+      n_in_hand = (pf_pla.y >> 8) & 0xffu;
+      n_active = (pf_pla.y >> 16) & 0xffu;
+      steps_taken = (pf_pla.z >> 8) & 0xffu;
+      lean_p = narrow && lean_player(pf_pla);
       stab = stnb;
-      stnb = mbits_of(hdn);
+      stnb = mbits_of(pf_hdn);
       pf_ok = false;
     }
     // the next turn change's records (the agent after ag1 and the player after it), read ahead
@@ -3988,8 +4022,10 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
       }
     }
     if (live && ended) {                                   // hand the env to k_env_fixup
+#ifndef COG_ISSUE_COUNT
       trio_store_private(s, i, R, selb);
       rngs[i] = srng;
+#endif
       park = (uint32_t)t | (finish ? kParkFinish : 0u);
       live = false;
     }
