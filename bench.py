@@ -519,10 +519,10 @@ def roofline(prof, n, k_chunk, launch_s, kind="trio", stamps=None, issue=None):
             "busy_ticks_per_step": busy,
             "note": "issue_frac = the stepping wave's per-step instructions (static count of its step loop without the "
                     "spin waits or the never-taken sampling fallback: an upper bound of what it issues) x a lone "
-                    "wave's cost per instruction of each kind when it has independent work (tools/r06/chainprobe.hip) "
+                    "wave's cost per instruction of each kind when it has independent work (tools/chainprobe.hip) "
                     "/ its measured busy ticks per step: near 1 = issue-bound, the chain at its floor; "
                     "dependent_chain_frac: the same with every instruction waiting for the one before "
-                    "(profiles/issue_profile.json, tools/r06/issue_frac.py, same engine source)"}
+                    "(profiles/issue_profile.json, tools/issue_frac.py, same engine source)"}
     pw = (e or {}).get("per_wave_step") or {}
     if pw.get("valu"):
         achieved = pw["valu"] * waves * k_chunk / launch_s
