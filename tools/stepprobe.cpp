@@ -1,6 +1,9 @@
 // Diagnostic only: the one-step-per-launch kernel (k_env_step<selected>, the runner at
 // set_chunk(1): what env.step() / runner.step() launch) on the bench workload.  Prints the
 // device us per launch (median of 200 launches, HIP events on the env's stream) per env count.
+// With tools/stepprobe_priv.patch applied to the engine (git apply; revert after the build) and
+// -DPROBE_PRIV_MODE=1 / 2 / 3: no state stores / the private stores as issued (AoS) / the same in a
+// structure-of-arrays layout, both into scratch (profiles/r06_step_store_probe.txt).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -mllvm -amdgpu-sched-strategy=max-ilp \
 //         -Iinclude -Igym-eldorado_amd/csrc tools/stepprobe.cpp -o tools/bin/stepprobe
 #include "../gym-eldorado_amd/csrc/cog_engine.hip"
