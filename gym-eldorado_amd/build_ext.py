@@ -57,9 +57,11 @@ HEADERS = [os.path.join(CSRC, f) for f in ("cog_engine.h", "cog_tables.h", "cog_
 
 def _compile_cmd(src, obj, defs=()):
     # max-ilp scheduling: the rollout runs one wave per SIMD, so only instruction-level
-    # parallelism hides latency (1 % faster than the default, tools/flags_exp.sh)
+    # parallelism hides latency (1 % faster than the default, tools/flags_exp.sh); loop heads on
+    # 64-B instruction-cache lines: the trio's step time otherwise moves by 1-2 % with unrelated
+    # code size changes (profiles/r06_compact_decks_ab.txt)
     return [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c",
-            "-ffp-contract=off", "-mllvm", "-amdgpu-sched-strategy=max-ilp", "-Wall",
+            "-ffp-contract=off", "-mllvm", "-amdgpu-sched-strategy=max-ilp", "-falign-loops=64", "-Wall",
             *defs, f"-I{INCLUDE}", f"-I{CSRC}", src, "-o", obj]
 
 

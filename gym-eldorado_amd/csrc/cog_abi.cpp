@@ -290,6 +290,11 @@ struct EnvShard {
   // K steps then needs no k_env_fixup (cog::launch_rollout's no_fixup; the kernel reports a park
   // anyway as an error, F_PARK_NOFIX).
   uint64_t lean_clock = ~0ull;
+  // The last launch that wrote decks was a trio rollout (+ its fix-up), so DevState::cdeck / cwide
+  // hold every env's decks and the next trio launch may load them instead of the DeckObs records
+  // (DevState::cdeck_ok).  Every other deck-writing call (reset, steps, the other rollouts, a
+  // device-record invalidation) clears it.
+  bool cdeck_ok = false;
 };
 
 struct cog_env {
@@ -435,7 +440,7 @@ void env_free(cog_env *e) {
   for (EnvShard &k : e->sh) {
     DeviceGuard g(k.device);
     if (k.stream) (void)hipStreamSynchronize(k.stream);
-    void *dev[] = {k.s.obs, k.outs, k.s.priv, k.s.grid, k.s.cgrid, k.s.heads, k.s.gen, k.s.dirty, k.d_actions, k.mir,
+    void *dev[] = {k.s.obs, k.outs, k.s.priv, k.s.grid, k.s.cgrid, k.s.heads, k.s.cdeck, k.s.cwide, k.s.gen, k.s.dirty, k.d_actions, k.mir,
                    k.s.park, k.s.parkq, k.done.ctr};
     for (void *p : dev)
       if (p) (void)hipFree(p);
@@ -645,6 +650,7 @@ int refresh_full(cog_env *e) {
 cog::DevState launch_state(const EnvShard &k, bool host_views) {
   cog::DevState s = k.s;
   if (!host_views) s.cap = 0;
+  s.cdeck_ok = k.cdeck_ok ? 1u : 0u;
   return s;
 }
 
@@ -693,7 +699,8 @@ int env_shard_init(EnvShard &k, uint32_t default_seed, uint32_t *err_word) {
       (rc = dmalloc(&s.gen, n * sizeof(cog::GenScratch))) || (rc = dmalloc(&s.dirty, n * sizeof(uint32_t))) ||
       (rc = dmalloc(&k.d_actions, n * COG_ACTION_BYTES)) || (rc = dmalloc(&s.park, n * sizeof(uint32_t))) ||
       (rc = dmalloc(&s.parkq, cog::park_list_bytes(n))) ||
-      (rc = dmalloc(&k.done.ctr, 256)) || (rc = zc_alloc(&k.h_outs, L.alloc)))
+      (rc = dmalloc(&k.done.ctr, 256)) || (rc = zc_alloc(&k.h_outs, L.alloc)) ||
+      (rc = dmalloc(&s.cdeck, n * 10 * sizeof(uint4))) || (rc = dmalloc(&s.cwide, n * sizeof(uint32_t))))
     return rc;
   std::memset(k.h_outs, 0, L.alloc);
   s.n = n;
@@ -819,6 +826,7 @@ static int env_reset_impl(cog_env *e, const cog::ResetParams &p) {
     k.done.queued = false;
     k.host_synced = false;                                 // (refresh_full: the mirror is rebuilt later)
     k.lean_clock = e->n_players >= 3 && e->max_steps ? 0ull : ~0ull;
+    k.cdeck_ok = false;
   }
   for (EnvShard &k : e->sh) {
     DeviceGuard g(k.device);
@@ -874,6 +882,7 @@ int cog_env_step_device_stream(cog_env *env, const void *d_actions, size_t n, vo
     HIPCHK(hipStreamWaitEvent(k.stream, k.ev, 0));
   }
   k.lean_clock = ~0ull;                                    // (arbitrary actions)
+  k.cdeck_ok = false;
   if (cog::launch_step(launch_state(k, env->host), static_cast<const uint8_t *>(d_actions), k.stream))
     return fail(COG_ERR_HIP, std::string("step launch failed: ") + hipGetErrorString(hipGetLastError()));
   return finish(env, true);
@@ -920,6 +929,7 @@ int cog_env_step(cog_env *env, const cog_action_t *actions, size_t n) {
     uint32_t seq = 0, *ctr = nullptr;
     k.pub_done = false;
     k.lean_clock = ~0ull;                                  // (arbitrary actions)
+    k.cdeck_ok = false;
     if (env->host && k.zc && k.mir_valid && k.host_synced && cog::step_pub_ok(k.n) &&
         (ctr = signal_arm(k.done, seq))) {                 // the step publishes and signals itself
       cog::DevState ps = launch_state(k, true);
@@ -1186,6 +1196,7 @@ int cog_env_invalidate_device(cog_env *env, void *stream) {
       HIPCHK(hipStreamWaitEvent(k.stream, k.ev, 0));
     }
     k.lean_clock = ~0ull;                                  // (edited masks or decks: any path)
+    k.cdeck_ok = false;
     if (cog::launch_resync(k.s, k.stream))
       return fail(COG_ERR_HIP, std::string("resync launch failed: ") + hipGetErrorString(hipGetLastError()));
   }
@@ -1200,6 +1211,7 @@ int cog_env_set_autoreset(cog_env *env, int on) {
   for (EnvShard &k : env->sh) {
     k.s.autoreset = on ? 1u : 0u;
     k.lean_clock = ~0ull;
+    k.cdeck_ok = false;
   }
   return COG_OK;
 }
@@ -1468,6 +1480,7 @@ static int runner_launch_fused(cog_runner *r, int steps) {
     // publishes itself, the sampled actions included (k_env_step_pub), as env.step() does
     if (host && steps == 1 && !r->timing && k.zc && k.mir_valid && k.host_synced && cog::step_pub_ok(k.n) && q.n) {
       k.lean_clock = ~0ull;                                // (a full step: not the trio)
+      k.cdeck_ok = false;
       uint8_t *h_act = const_cast<uint8_t *>(zc_device(r->smp->h_actions + q.first, q.n * COG_ACTION_BYTES));
       uint32_t seq = 0, *ctr = nullptr;
       if (h_act && zc_same_on(k.device, r->smp->h_actions + q.first) && (ctr = signal_arm(k.done, seq))) {
@@ -1495,13 +1508,20 @@ static int runner_launch_fused(cog_runner *r, int steps) {
         // no env can park in this launch (EnvShard::lean_clock): no fix-up launch
         const bool no_fixup = trio && k.s.autoreset && k.lean_clock != ~0ull &&
                               k.lean_clock + (uint64_t)kk < (uint64_t)r->env->max_steps;
-        if (cog::launch_rollout(s, src, kk, q.d_rng, q.d_actions, k.stream, r->env->n_players >= 3, &k.park_seq,
+        cog::DevState sc = s;
+        sc.cdeck_ok = trio && k.cdeck_ok ? 1u : 0u;
+#ifdef COG_NO_CDECK                                        // (A/B probe builds: the DeckObs loads always)
+        sc.cdeck_ok = 0u;
+#endif
+        if (cog::launch_rollout(sc, src, kk, q.d_rng, q.d_actions, k.stream, r->env->n_players >= 3, &k.park_seq,
                                 no_fixup))
           return fail(COG_ERR_HIP, std::string("rollout launch failed: ") + hipGetErrorString(hipGetLastError()));
         k.lean_clock = trio && k.lean_clock != ~0ull ? k.lean_clock + (uint64_t)kk : ~0ull;
+        k.cdeck_ok = trio;                                 // (the trio and its fix-up write cdeck)
       }
     } else {
       k.lean_clock = ~0ull;                                // (full steps)
+      k.cdeck_ok = false;
       for (int t = 0; t < steps; t++)
         if (cog::launch_sample_step(s, src, q.d_rng, q.d_actions, k.stream))
           return fail(COG_ERR_HIP, std::string("sample_step launch failed: ") + hipGetErrorString(hipGetLastError()));
@@ -1538,6 +1558,7 @@ int cog_runner_step(cog_runner *r) {
     EnvShard &k = r->env->sh[j];
     DeviceGuard g(k.device);
     k.lean_clock = ~0ull;                                  // (a full step)
+    k.cdeck_ok = false;
     if (cog::launch_step(launch_state(k, host), r->smp->sh[j].d_actions, k.stream))
       return fail(COG_ERR_HIP, std::string("step launch failed: ") + hipGetErrorString(hipGetLastError()));
   }

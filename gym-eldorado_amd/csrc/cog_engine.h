@@ -95,6 +95,14 @@ struct DevState {
   uint8_t *grid;
   uint8_t *cgrid;                    // [n] x 2304 B compact 48x48 hex codes (lookups + encode)
   uint4 *heads;                      // [n][5] mask bit-vectors: selected, stored of players 0..3
+  // the trio drawing wave's compact deck image as of the end of the last trio launch (+ its
+  // fix-up): [n][10] granules = players 0..3 x the five DeckObs piles of types 0-7 (8 B each,
+  // deck_expand / compact_of), and [n] a word that is 1 when an env's deck held a type >= 8 (not
+  // representable: that env parks at step 0).  cdeck_ok (the host's EnvShard::cdeck_ok): no launch
+  // since wrote a deck without writing them, so a trio launch loads these 164 B instead of the
+  // four 112-B DeckObs records (about a third of its prologue's HBM bytes at the line granularity)
+  uint4 *cdeck;
+  uint32_t *cwide;
   GenScratch *gen;
   uint32_t *status;                  // [0] OR of error flags, [1] error count, [2] dirty count
   uint32_t *dirty;                   // [cap] local indices of envs whose map was re-generated
@@ -115,6 +123,7 @@ struct DevState {
   uint32_t park_par;
   uint32_t no_fixup;                 // 1: no k_env_fixup follows this launch (a park is an error)
   uint32_t trio_jt;                  // 1: the trio launch of at most one workgroup per CU (its LAT form)
+  uint32_t cdeck_ok;                 // 1: cdeck / cwide hold every env's decks (see above)
   // direct publish (launch_step_pub only; null otherwise): device addresses of the shard's pinned
   // ObsData view and outs block, and the publish mirror (k_publish's `mir`)
   uint8_t *pub_obs, *pub_outs, *pub_mir;

@@ -2773,6 +2773,8 @@ DEV DevState wave_view(const DevState &s, size_t base) {
   v.grid += base * (size_t)kGridBytes;
   v.cgrid += base * COG_CELLS;
   v.heads += 5 * base;
+  v.cdeck += 10 * base;
+  v.cwide += base;
   v.gen += base;
   v.park += base;
   v.first += base;
@@ -4093,8 +4095,8 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
   constexpr bool lat = LAT;                                // (the acting player's counters: trio_stepper)
   uint4 shb0 = make_uint4(0u, 0u, 0u, 0u);                 // ObsData 16128.. as stored: the phase
   uint32_t infob = 0u;                                     // dword and the resources; Info steps
-  if (live) {
-#pragma unroll
+  if (live && !s_glob.cdeck_ok) {                          // the DeckObs records (else storing wave A
+#pragma unroll                                             // loads the compact image the last launch left)
     for (int p = 0; p < 4; p++) {
       const uint4 *src = reinterpret_cast<const uint4 *>(deck_ptr(s, i, p));
       uint4 dk[7];
@@ -4105,11 +4107,13 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
 #pragma unroll
       for (int q = 0; q < 5; q++) D.img[p][q][l] = pile[q];
     }
+  }
+  if (live) {
     rng = reinterpret_cast<const uint32_t *>(s.priv + i)[0];
     infob = reinterpret_cast<const uint32_t *>(s.priv + i)[12];   // EnvPriv granule 3, dword 0
     shb0 = reinterpret_cast<const uint4 *>(s.obs + i * COG_OBS_BYTES + COG_OBS_PHASE)[0];
   }
-  D.wide[l] = narrow ? 0u : 1u;                            // (a wide env: the stepper parks it at step 0)
+  if (!s_glob.cdeck_ok) D.wide[l] = narrow ? 0u : 1u;      // (a wide env: the stepper parks it at step 0)
   uint32_t flags = 0u;                                     // hazard flags of the draws
   __builtin_amdgcn_s_waitcnt(0);
   TL(15);                                                  // (timeline: this wave's prologue done)
@@ -4262,11 +4266,23 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
       const uint4 g1 = pv4[1];
       const uint32_t w[5] = {sh1.x, sh1.y, sh1.z, sh1.w, sh2.x};
       E.avail = shop_avail_of(w, (g1.y >> 8) & 0xffu, g1.z);   // (no purchase in the lean step: fixed)
+      if (s_glob.cdeck_ok) {                               // the drawing wave's compact decks as the
+        const uint4 *src = s.cdeck + 10 * i;               // last launch left them (DevState::cdeck)
+        uint4 c[10];
+#pragma unroll
+        for (int g = 0; g < 10; g++) c[g] = src[g];
+#pragma unroll
+        for (int g = 0; g < 10; g++) {                     // entries 2g, 2g + 1 of [player][pile]
+          D.img[(2 * g) / 5][(2 * g) % 5][l] = make_uint2(c[g].x, c[g].y);
+          D.img[(2 * g + 1) / 5][(2 * g + 1) % 5][l] = make_uint2(c[g].z, c[g].w);
+        }
+      }
     } else {
       selb = mbits_of(s.heads[5 * i]);
       x = rngs_glob[wbase + (size_t)l];
     }
   }
+  if (PART == 0 && s_glob.cdeck_ok) D.wide[l] = live ? s.cwide[i] : 0u;   // (else the drawing wave's)
   if (PART == 1) {                                         // steps 0..3 from the state at step 0
 #pragma unroll
     for (int k = 0; k < kTrioLead; k++) {
@@ -4377,6 +4393,13 @@ DEV uint32_t trio_storer(TrioLds &D, const DevState &s_glob, int steps, int epw,
     if (live) {
 #pragma unroll
       for (int p = 0; p < 4; p++) D.heads[p][l] = D.stbA[p][l];
+      uint4 *dst = s.cdeck + 10 * i;                       // the drawing wave's final decks (it is past
+#pragma unroll                                             // the last record) for the next launch; a
+      for (int g = 0; g < 10; g++) {                       // parked env's: k_env_fixup rewrites them
+        const uint2 a = D.img[(2 * g) / 5][(2 * g) % 5][l], b = D.img[(2 * g + 1) / 5][(2 * g + 1) % 5][l];
+        dst[g] = make_uint4(a.x, a.y, b.x, b.y);
+      }
+      s.cwide[i] = D.wide[l];
     }
   }
   PH_FLUSH(s_glob);
@@ -4444,6 +4467,20 @@ __global__ void __launch_bounds__(64) k_env_fixup(DevState s, int steps, uint32_
         reinterpret_cast<uint2 *>(pw + 8)[p] = L.cells[p][l];
         s.heads[5 * i0 + 1 + p] = L.heads[p][l];
       }
+      bool narrow = true;                                  // the trio's compact decks (DevState::cdeck)
+#pragma unroll                                             // from the records this lane just stored
+      for (int p = 0; p < 4; p++) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(deck_ptr(s, i0, p));
+        uint4 dk[7];
+        uint2 pile[5];
+#pragma unroll
+        for (int k = 0; k < 7; k++) dk[k] = src[k];
+        narrow = compact_of(dk, pile) && narrow;
+        uint2 *dst = reinterpret_cast<uint2 *>(s.cdeck + 10 * i0) + 5 * p;
+#pragma unroll
+        for (int q = 0; q < 5; q++) dst[q] = pile[q];
+      }
+      s.cwide[i0] = narrow ? 0u : 1u;
       s.park[i0] = kParkNone;
     }
   }

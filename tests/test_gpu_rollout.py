@@ -288,3 +288,40 @@ def test_trio_deferred_turn_end_redo_path(cg, tmp_path, max_steps):
                        text=True, timeout=240, env=dict(os.environ, COG_DEBUG_REDO_STEP="7"))
     assert r.returncode == 0, r.stderr[-3000:]
     assert r.stdout.strip().splitlines()[-1].startswith("OK")
+
+
+@pytest.mark.parametrize("n", [4096, 40960])
+def test_trio_compact_decks_across_drivers(cg, n):
+    """A trio launch starts from the compact deck image the previous trio launch (and its fix-up)
+    left (DevState::cdeck / cwide), which holds only while trio launches alone wrote decks.  Here
+    full-dynamics launches (moves and purchases: decks with types >= 8, which the compact form
+    cannot hold, so those envs park at step 0 of every trio launch) alternate with selected-mask
+    trio launches of 20 steps, and the result must equal the oracle running the same drivers.
+    4,096 envs: the LAT trio and the duo; 40,960: two trio workgroups per CU and the one-wave
+    kernel."""
+    seed = 2468
+    env = cg.vec.get_vec_env(n)()
+    smp = cg.vec.get_vec_sampler(n)(seed)
+    env.reset(seed, 4, 3, cg.Difficulty(2), 100000, False)
+    sel = cg.vec.get_runner(n)(env, smp, None, device_views=True)
+    sto = cg.vec.get_runner(n)(env, smp, None, stored_masks=True, device_views=True)
+    sel.set_chunk(20)
+    sto.set_chunk(50)
+    orc, osm = po.OracleVec(n), po.OracleSampler(n, seed)
+    orc.reset(seed, 4, 3, 2, 100000)
+    for kind, k in (("sel", 40), ("sto", 150), ("sel", 60), ("sto", 50), ("sel", 40)):
+        (sel if kind == "sel" else sto).rollout(k)
+        for _ in range(k):
+            osm.sample(orc.selected_action_masks if kind == "sel" else po.stored_masks(orc))
+            orc.step(osm.actions)
+    sel.sync()
+    sto.sync()
+    env.sync_host()
+    for nm in ("observations", "selected_action_masks", "infos"):
+        bad = po.named_equal(getattr(env, nm), getattr(orc, nm))
+        assert bad is None, f"{nm}.{bad} differs from the oracle"
+    for nm in ("rewards", "dones", "agent_selection"):
+        assert np.array_equal(getattr(env, nm), getattr(orc, nm)), nm
+    piles = np.ascontiguousarray(orc.observations["player_data"]["obs"]).view(np.uint8).reshape(n, 4, 5, 21)
+    wide = int((piles[:, :, :, 8:] != 0).any(axis=(1, 2, 3)).sum())   # (draw, hand, active, played, discard)
+    assert wide > 0, "no deck holds a type >= 8: the test lost its case"

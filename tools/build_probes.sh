@@ -5,7 +5,7 @@
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p tools/bin
-F="-O3 -std=c++17 -ffp-contract=off -mllvm -amdgpu-sched-strategy=max-ilp -Iinclude -Igym-eldorado_amd/csrc"
+F="-O3 -std=c++17 -ffp-contract=off -mllvm -amdgpu-sched-strategy=max-ilp -falign-loops=64 -Iinclude -Igym-eldorado_amd/csrc"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 $F tools/duoprobe.cpp -o tools/bin/duoprobe 2>/dev/null &
 /opt/rocm/bin/hipcc --offload-arch=gfx950 $F -DCOG_STAMPS tools/duoprobe.cpp -o tools/bin/duoprobe_st 2>/dev/null &
 wait
