@@ -4074,6 +4074,81 @@ DEV void trio_stepper(TrioLds &D, const DevState &s_glob, int steps, int epw, ui
   PH_FLUSH(s_glob);
 }
 
+// One record's play on the drawing wave (trio_drawer; round 6): the acting player's counters
+// (LAT), the ObsData phase / resources granule, the Info steps byte and Deck::activate's hand /
+// active piles, on the values the caller read (p4: D.pl[ag], h / a: D.img[ag][1 / 2]), which it
+// updates and stores back; selects instead of exec-mask branches for the common path.
+template <bool LAT>
+DEV void trio_draw_play(TrioLds &D, const DevState &s, int l, bool live, int slot, uint32_t mt, uint32_t w2,
+                        uint32_t gx, uint4 &p4, uint2 &h, uint2 &a, uint4 &shb0, uint32_t &infob, bool &te,
+                        bool &rec_out, uint32_t &dm, uint32_t &nact) {
+  const size_t i = (size_t)l;
+  const int ag = (int)((mt >> 2) & 3u);
+  const bool valid = live && (mt & kMetaValid);
+  const bool rec = valid && (mt & kMetaStepped);
+  rec_out = rec;
+  te = rec && (int)(mt >> 24) != ag;
+  const uint32_t a_play = w2 & 0xffu;
+  const bool play = rec && a_play != 0u;
+  const int c = (int)((a_play - 1u) & 7u);               // (c < 8: the stepping wave parks any other type)
+  if (LAT) {                                             // the acting player's counters (PlayerPriv:
+    uint4 q = p4;                                        // steps_taken, n_in_hand, n_active, idx_last;
+    uint32_t na = (q.y >> 16) & 0xffu;                   // Player::play_card, player.cpp:45-60; u8)
+    q.z = (q.z & 0xffff00ffu) | (((q.z >> 8) + 1u) & 0xffu) << 8;
+    q.y = play ? (q.y & 0xffff00ffu) | ((((q.y >> 8) & 0xffu) - 1u) & 0xffu) << 8 : q.y;
+    na = play ? (na + 1u) & 0xffu : na;
+    q.z = play ? (q.z & ~0xffu) | (a_play - 1u) : q.z;
+    na = te ? 0u : na;                                   // Player::end_turn
+    q.y = (q.y & 0xff00ffffu) | na << 16;
+    p4.x = rec ? q.x : p4.x;                             // (component selects: a select of two
+    p4.y = rec ? q.y : p4.y;                             // vectors compiles to one of two addresses
+    p4.z = rec ? q.z : p4.z;                             // in scratch)
+    if (rec) D.pl[ag][l] = p4;
+    nact = rec ? na : 0u;
+  }
+  // the ObsData phase / resources granule and the Info byte (the stepping wave leaves the resources
+  // and the counts to this wave)
+  infob = rec ? (infob & ~(0xffu << (8 * ag))) | ((((infob >> (8 * ag)) + 1u) & 0xffu) << (8 * ag)) : infob;
+  uint32_t phase = shb0.x & 0xffu;
+  phase = phase == COG_PHASE_INACTIVE ? (uint32_t)COG_PHASE_MOVEMENT : phase;
+  const bool mv = play && phase == COG_PHASE_MOVEMENT, buy = play && phase == COG_PHASE_BUYING;
+  const uint32_t coin = cardf(kRes2, c);                 // Player::play_card (player.cpp:45-60)
+  uint4 g0 = shb0;
+  g0.y = mv ? __float_as_uint((float)cardf(kRes0, c)) : g0.y;
+  g0.z = mv ? __float_as_uint((float)cardf(kRes1, c)) : g0.z;
+  const float bw = __uint_as_float(g0.w) + (coin > 0 ? (float)coin : 0.5f);
+  g0.w = mv ? __float_as_uint((float)coin) : buy ? __float_as_uint(bw) : g0.w;
+  g0.y = te ? 0u : g0.y;                                 // Player::end_turn (+0.f)
+  g0.z = te ? 0u : g0.z;
+  g0.w = te ? 0u : g0.w;
+  g0.x = rec ? gx : g0.x;
+  if (valid) {
+    reinterpret_cast<uint3 *>(&D.ring[slot][0][l].y)[0] = make_uint3(g0.y, g0.z, g0.w);   // (storing wave A)
+    s.info[i * COG_INFO_BYTES + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag] = (uint8_t)(infob >> (8 * ag));
+    if (ne4(g0, shb0)) reinterpret_cast<uint4 *>(s.obs + i * COG_OBS_BYTES + COG_OBS_PHASE)[0] = g0;
+  }
+  shb0.x = valid ? g0.x : shb0.x;
+  shb0.y = valid ? g0.y : shb0.y;
+  shb0.z = valid ? g0.z : shb0.z;
+  shb0.w = valid ? g0.w : shb0.w;
+  // Deck::activate (cards.cpp:242-253): hand[c]--, active[c]++ (u8)
+  const uint32_t sh = 8u * (uint32_t)(c & 3);
+  uint32_t hw = c < 4 ? h.x : h.y, aw = c < 4 ? a.x : a.y;
+  hw = (hw & ~(0xffu << sh)) | ((((hw >> sh) - 1u) & 0xffu) << sh);
+  aw = (aw & ~(0xffu << sh)) | ((((aw >> sh) + 1u) & 0xffu) << sh);
+  const bool lo = c < 4;
+  h.x = play && lo ? hw : h.x;
+  h.y = play && !lo ? hw : h.y;
+  a.x = play && lo ? aw : a.x;
+  a.y = play && !lo ? aw : a.y;
+  if (play) {
+    D.img[ag][1][l] = h;
+    D.img[ag][2][l] = a;
+  }
+  const int bh = COG_DECK_HAND + c, ba = COG_DECK_ACTIVE + c;   // the record's granules
+  dm = play ? 1u << (bh >> 4) | 1u << (ba >> 4) : 0u;
+}
+
 // The drawing wave keeps every player's deck (img).  It takes records in pairs r, r + 1 (r even):
 // each record's play replayed on the acting player's deck (the hand and active piles, as
 // Deck::activate does); then one pass over the turn ends of either record (discard + draws,
@@ -4129,64 +4204,30 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
     uint32_t dm[2] = {0u, 0u}, nact[2] = {0u, 0u};
     int agj[2] = {0, 0};
     bool te[2] = {false, false}, recj[2] = {false, false};
-#pragma unroll
-    for (int j = 0; j < 2; j++) {                          // the plays, in record order
-      if (j >= nrec) continue;                             // (uniform)
-      const uint32_t meta = D.ring[slot[j]][1][l].w;
-      const int ag = (int)((meta >> 2) & 3u);
-      const bool rec = live && (meta & kMetaValid) && (meta & kMetaStepped);
-      agj[j] = ag;
-      recj[j] = rec;
-      te[j] = rec && (int)(meta >> 24) != ag;
-      const int a_play = (int)(D.ring[slot[j]][2][l].w & 0xffu);
-      if (rec && lat) {                                    // the acting player's counters (PlayerPriv:
-        uint4 p4 = D.pl[ag][l];                            // steps_taken, n_in_hand, n_active, idx_last;
-        uint32_t na = (p4.y >> 16) & 0xffu;                // Player::play_card, player.cpp:45-60; u8)
-        p4.z = (p4.z & 0xffff00ffu) | (((p4.z >> 8) + 1u) & 0xffu) << 8;
-        if (a_play) {
-          p4.y = (p4.y & 0xffff00ffu) | ((((p4.y >> 8) & 0xffu) - 1u) & 0xffu) << 8;
-          na = (na + 1u) & 0xffu;
-          p4.z = (p4.z & ~0xffu) | (uint32_t)(a_play - 1);
-        }
-        if (te[j]) na = 0u;                                // Player::end_turn
-        p4.y = (p4.y & 0xff00ffffu) | na << 16;
-        D.pl[ag][l] = p4;
-        nact[j] = na;
+    // (round 6: both records' words, and both acting players' counters, hand and active piles, read
+    // at once -- a second record of the same player continues from the first one's values in
+    // registers -- and the common path computed with selects, not exec-mask branches)
+    const uint32_t mt0 = D.ring[slot[0]][1][l].w, w20 = D.ring[slot[0]][2][l].w, gx0 = D.ring[slot[0]][0][l].x;
+    uint32_t mt1 = D.ring[slot[1]][1][l].w;                // (a slot past nrec: read, not used)
+    const uint32_t w21 = D.ring[slot[1]][2][l].w, gx1 = D.ring[slot[1]][0][l].x;
+    if (nrec < 2) mt1 = 0u;                                // (uniform: no second record)
+    const int ag0 = (int)((mt0 >> 2) & 3u), ag1 = (int)((mt1 >> 2) & 3u);
+    uint4 p0 = make_uint4(0u, 0u, 0u, 0u), p1 = p0;
+    if (lat) {
+      p0 = D.pl[ag0][l];
+      p1 = D.pl[ag1][l];
+    }
+    uint2 h0 = D.img[ag0][1][l], a0 = D.img[ag0][2][l], h1 = D.img[ag1][1][l], a1 = D.img[ag1][2][l];
+    trio_draw_play<lat>(D, s, l, live, slot[0], mt0, w20, gx0, p0, h0, a0, shb0, infob, te[0], recj[0], dm[0], nact[0]);
+    agj[0] = ag0;
+    if (nrec > 1) {                                        // (uniform)
+      if (ag1 == ag0) {                                    // the same player: record 0's values
+        p1.x = p0.x; p1.y = p0.y; p1.z = p0.z; p1.w = p0.w;
+        h1.x = h0.x; h1.y = h0.y;
+        a1.x = a0.x; a1.y = a0.y;
       }
-      if (live && (meta & kMetaValid)) {                   // the ObsData phase / resources granule and
-        uint4 g0 = shb0;                                   // the Info byte (the stepping wave leaves
-        if (rec) {                                         // the resources and the counts to this wave)
-          infob = (infob & ~(0xffu << (8 * ag))) | ((((infob >> (8 * ag)) + 1u) & 0xffu) << (8 * ag));
-          uint32_t phase = shb0.x & 0xffu;
-          if (phase == COG_PHASE_INACTIVE) phase = COG_PHASE_MOVEMENT;
-          if (a_play) {                                    // Player::play_card (player.cpp:45-60)
-            const int c = a_play - 1;
-            if (phase == COG_PHASE_MOVEMENT) {
-              g0.y = __float_as_uint((float)cardf(kRes0, c));
-              g0.z = __float_as_uint((float)cardf(kRes1, c));
-              g0.w = __float_as_uint((float)cardf(kRes2, c));
-            } else if (phase == COG_PHASE_BUYING) {
-              const uint32_t coin = cardf(kRes2, c);
-              g0.w = __float_as_uint(__uint_as_float(g0.w) + (coin > 0 ? (float)coin : 0.5f));
-            }
-          }
-          if (te[j]) g0.y = g0.z = g0.w = 0u;              // Player::end_turn (+0.f)
-          g0.x = D.ring[slot[j]][0][l].x;
-        }
-        reinterpret_cast<uint3 *>(&D.ring[slot[j]][0][l].y)[0] = make_uint3(g0.y, g0.z, g0.w);   // (storing wave A)
-        s.info[i * COG_INFO_BYTES + COG_AGENT_INFO0 + COG_AGENT_INFO_STRIDE * ag] = (uint8_t)(infob >> (8 * ag));
-        if (ne4(g0, shb0)) reinterpret_cast<uint4 *>(s.obs + i * COG_OBS_BYTES + COG_OBS_PHASE)[0] = g0;
-        shb0 = g0;
-      }
-      if (rec && a_play) {                                 // Deck::activate (cards.cpp:242-253): hand[c]--,
-        const int c = a_play - 1;                          // active[c]++ (u8; c < 8: the stepping wave
-        uint8_t *ph = reinterpret_cast<uint8_t *>(&D.img[ag][1][l]) + c;   // parks any other type)
-        uint8_t *pa = reinterpret_cast<uint8_t *>(&D.img[ag][2][l]) + c;
-        *ph = (uint8_t)(*ph - 1u);
-        *pa = (uint8_t)(*pa + 1u);
-        const int bh = COG_DECK_HAND + c, ba = COG_DECK_ACTIVE + c;   // the record's granules
-        dm[j] |= 1u << (bh >> 4) | 1u << (ba >> 4);
-      }
+      trio_draw_play<lat>(D, s, l, live, slot[1], mt1, w21, gx1, p1, h1, a1, shb0, infob, te[1], recj[1], dm[1], nact[1]);
+      agj[1] = ag1;
     }
     const bool any = te[0] || te[1];                       // (at most one of them)
     if (__builtin_amdgcn_ballot_w64(any) && any) {         // the turn end's discard + draws

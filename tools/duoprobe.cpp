@@ -83,7 +83,7 @@ int main(int argc, char **argv) {
       const char *store_names[16] = {"", "", "", "", "", "wait Y / B: wait record", "A: wait drawn / B: wait drawn",
                                      "wait X / B: front cursor work", "", "", "", "", "", "stores (the drawn record's)",
                                      "", ""};
-      const char *draw_names[16] = {"", "", "", "", "", "", "", "", "wait: records", "plays + turn-end draws", "", "", "",
+      const char *draw_names[16] = {"", "", "", "", "", "", "", "plays", "wait: records", "turn-end pass + ring words", "", "", "",
                                     "", "", ""};
       // the trio's stepping wave (trio_stepper): 2 = the loop top's waits (ring slot, presampled
       // draws), 5 = the turn change's wait for the drawing wave; the rest is its own work
