@@ -4229,6 +4229,7 @@ DEV uint32_t trio_drawer(TrioLds &D, const DevState &s_glob, int steps, int epw)
       trio_draw_play<lat>(D, s, l, live, slot[1], mt1, w21, gx1, p1, h1, a1, shb0, infob, te[1], recj[1], dm[1], nact[1]);
       agj[1] = ag1;
     }
+    PH(7);                                                 // (stamps: the plays)
     const bool any = te[0] || te[1];                       // (at most one of them)
     if (__builtin_amdgcn_ballot_w64(any) && any) {         // the turn end's discard + draws
       const int j = te[1] ? 1 : 0, sl = te[1] ? slot[1] : slot[0], ag = te[1] ? agj[1] : agj[0];
