@@ -1,12 +1,14 @@
 """Diagnostic: steady full dynamics (stored masks, max_steps 100,000) at 65,536 envs with each
 rollout kernel ($COG_ROLLOUT is read once per process: one kernel per run).
-    COG_ROLLOUT=wave|pipe|duo python tools/fd_kinds.py [envs]"""
+    COG_ROLLOUT=wave|pipe|duo python tools/fd_kinds.py [envs]
+$COG_PKG: the directory holding the city_of_gold package to load (a same-box A/B against another
+engine build; default gym-eldorado_amd)."""
 import os
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "gym-eldorado_amd"))
+sys.path.insert(0, os.environ.get("COG_PKG") or os.path.join(ROOT, "gym-eldorado_amd"))
 import city_of_gold as cg  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
@@ -23,5 +25,5 @@ r.rollout(2000)
 r.sync()
 wall = time.perf_counter() - t0
 ms, k = r.kernel_time()
-print("%s n=%d  %.3f us/step wall, %.3f us/step device  %.3g env-steps/s" % (
-    os.environ.get("COG_ROLLOUT", "auto"), n, wall / 2000 * 1e6, ms * 1e3 / max(k, 1), n * 2000 / wall))
+print("%s%s n=%d  %.3f us/step wall, %.3f us/step device  %.3g env-steps/s" % (
+    os.environ.get("COG_ROLLOUT", "auto"), " [%s]" % os.environ["COG_PKG"] if os.environ.get("COG_PKG") else "", n, wall / 2000 * 1e6, ms * 1e3 / max(k, 1), n * 2000 / wall))

@@ -2,6 +2,7 @@
 // boundaries of env_step_lane) on the bench workload; prints mean cycles per phase.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DCOG_STAMPS -Iinclude \
 //         -Igym-eldorado_amd/csrc tools/stamp_step.cpp -o tools/stamp_step
+//   tools/stamp_step N STEPS CHUNK [STORED]   (STORED=1: the full-dynamics driver, stored masks)
 #include "../gym-eldorado_amd/csrc/cog_engine.hip"
 #include "../gym-eldorado_amd/csrc/cog_abi.cpp"
 #include <cstdio>
@@ -12,11 +13,12 @@ int main(int argc, char **argv) {
   const size_t n = argc > 1 ? strtoul(argv[1], nullptr, 10) : 65536;
   const int steps = argc > 2 ? atoi(argv[2]) : 50;
   const int chunk = argc > 3 ? atoi(argv[3]) : 1;   // > 1: the persistent rollout, per-phase totals
+  const bool stored = argc > 4 && atoi(argv[4]) != 0;  // 1: full dynamics (stored masks, the wave kernel)
   cog_env *env;
   cog_sampler *smp;
   cog_runner *run;
   if (cog_env_create(n, 0, &env) || cog_sampler_create(n, 12345, 0, &smp) ||
-      cog_env_reset(env, 12345, 4, 3, 2, 100000, 0) || cog_runner_create(env, smp, 1, COG_RUNNER_DEVICE_VIEWS, &run)) {
+      cog_env_reset(env, 12345, 4, 3, 2, 100000, 0) || cog_runner_create(env, smp, 1, COG_RUNNER_DEVICE_VIEWS | (stored ? COG_RUNNER_STORED_MASKS : 0u), &run)) {
     printf("setup failed: %s\n", cog_last_error());
     return 1;
   }
